@@ -1,0 +1,188 @@
+/*
+ * bann.h — C ABI of the MI355X-native branch-network HMC hot path.
+ *
+ * Drop-in boundary for the per-branch math of medical-genomics-group/rs-bann
+ * (Rust + ArrayFire).  The reference has no FFI: its hot path sits behind the
+ * Rust traits BranchSampler (src/net/branch/branch_sampler.rs:32-1300) and
+ * BranchStruct (src/net/branch/branch_struct.rs:119-141) and reaches the device
+ * through ArrayFire calls.  Each entry point below names the reference item it
+ * replaces (file:line).  A Rust binding is sketched in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every function returns BANN_OK (0) or a negative bann_status; the message
+ *    of the last failure is available from bann_last_error().
+ *  - Pointers are HOST pointers unless the name ends in _device.  They are read
+ *    or written synchronously inside the call and never retained.
+ *  - Parameter vectors use the reference param_vec order (params.rs:700-715):
+ *    all weights layer by layer, each (in x out) matrix column-major
+ *    (element (j,k) at k*in + j), then all biases.  num_params(b) floats.
+ *  - Precision vectors use the BranchPrecisions::param_vec order
+ *    (params.rs:272-289): weight precisions layer by layer (ARD priors: one per
+ *    input node for layers 0..L-2 and one for the output layer; base priors and
+ *    std-normal: one per layer), then the L-1 bias precisions, then the error
+ *    precision.  num_precisions(b) floats.
+ *  - A context owns one HIP device, one stream and all device buffers.  It is
+ *    not thread-safe; use one context per GPU (one process per GPU for
+ *    multi-GPU runs).
+ */
+#ifndef BANN_H
+#define BANN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bann_ctx bann_ctx;
+
+typedef enum {
+  BANN_OK = 0,
+  BANN_E_HIP = -1,    /* HIP runtime error (no device, launch failure, ...) */
+  BANN_E_SHAPE = -2,  /* inconsistent sizes / indices                        */
+  BANN_E_OOM = -3,    /* device allocation failed                            */
+  BANN_E_STATE = -4,  /* call order violated (e.g. compute before finalize)  */
+  BANN_E_ARG = -5     /* invalid argument value                              */
+} bann_status;
+
+/* activation_functions.rs:6-12 (same discriminants) */
+typedef enum { BANN_TANH = 0, BANN_RELU = 1, BANN_LEAKY_RELU = 2, BANN_SILU = 3, BANN_IDENTITY = 4 } bann_activation;
+
+/* one code per BranchSampler impl (model_type.rs:6-13) */
+typedef enum {
+  BANN_RIDGE_ARD = 0,   /* ridge_ard.rs   */
+  BANN_RIDGE_BASE = 1,  /* ridge_base.rs  */
+  BANN_LASSO_ARD = 2,   /* lasso_ard.rs   */
+  BANN_LASSO_BASE = 3,  /* lasso_base.rs  */
+  BANN_STD_NORMAL = 4   /* std_normal_branch.rs */
+} bann_prior;
+
+/* HMCStepResult (branch_sampler.rs:1310-1314) */
+typedef enum { BANN_ACCEPTED = 0, BANN_REJECTED = 1, BANN_REJECTED_EARLY = 2 } bann_hmc_status;
+
+/* StepSizeMode (mcmc_cfg.rs:264-270); INJECTED = caller supplies eps */
+typedef enum { BANN_STEP_UNIFORM = 0, BANN_STEP_RANDOM = 1, BANN_STEP_IZMAILOV = 3, BANN_STEP_INJECTED = 100 } bann_step_mode;
+
+/* ---------------- context ---------------- */
+int bann_ctx_create(int device, bann_ctx** out);
+int bann_ctx_destroy(bann_ctx* ctx);
+const char* bann_last_error(const bann_ctx* ctx);
+/* library build/version string; callable without a device */
+const char* bann_version(void);
+
+/* ---------------- genotypes: replaces GroupedGenotypes / BedVM ----------------
+ * genotypes.rs:7-12,44-48 (x_group_af), bed.rs:193-245 (from_file + column
+ * stats), bed.rs:325-355 (get_submatrix_af_standardized).  The matrix stays
+ * resident on the device as int8 genotypes; standardization (g - mu)/sigma
+ * with the population std (bed.rs:231-242) is folded into the kernels. */
+
+/* g: variant-major int8 genotypes g[j*n + i] in {0,1,2}; mu/sigma computed on device */
+int bann_genotypes_upload(bann_ctx* ctx, const int8_t* g, int64_t n, int64_t num_markers);
+/* payload: variant-major .bed bytes without the 3-byte signature (bed.rs:100-116),
+ * ceil(n/4) bytes per marker; decoded on the device with the 2-bit LUT of
+ * bed_lookup_tables.rs:4 (00->2, 01->0, 10->1, 11->0) */
+int bann_genotypes_upload_bed(bann_ctx* ctx, const uint8_t* payload, int64_t n, int64_t num_markers);
+/* synthetic cohort generated on the device: g_ij ~ Binomial(2, p_j),
+ * p_j ~ U(0.01, 0.5) (bed.rs:136-188 semantics; counter-based RNG, not the
+ * reference's ChaCha stream).  Zero-variance markers are redrawn. */
+int bann_genotypes_synthetic(bann_ctx* ctx, int64_t n, int64_t num_markers, uint64_t seed);
+int bann_genotypes_stats(bann_ctx* ctx, float* mu, float* sigma);
+/* override the standardization constants (e.g. statistics of a reference
+ * cohort, or mu = 0, sigma = 1 for pre-standardized / raw inputs); before finalize */
+int bann_genotypes_set_stats(bann_ctx* ctx, const float* mu, const float* sigma);
+/* copy genotypes of markers snp_idx[0..m) back to the host as g[j*n + i] */
+int bann_genotypes_download(bann_ctx* ctx, const int32_t* snp_idx, int32_t m, int8_t* g_out);
+
+/* ---------------- branches: replaces BranchCfg -> B::from_cfg ----------------
+ * branch_struct.rs:12-29 (from_cfg), branch_cfg.rs:185-193 (BranchCfg). */
+
+/* Adds a branch over markers snp_idx[0..m) (groups may overlap, external.rs).
+ * layer_widths: hidden..., summary, 1 (params.rs:470); num_layers >= 2.
+ * Returns the branch index (>= 0) or a negative bann_status. */
+int bann_branch_add(bann_ctx* ctx, const int32_t* snp_idx, int32_t m, const int32_t* layer_widths,
+                    int32_t num_layers, int32_t activation, int32_t prior);
+/* packs every branch's genotype block into the device layout; after this the
+ * branch set is fixed.  free_raw != 0 releases the full genotype matrix. */
+int bann_finalize(bann_ctx* ctx, int32_t free_raw);
+int bann_num_branches(const bann_ctx* ctx);
+int64_t bann_num_params(const bann_ctx* ctx, int32_t b);
+int64_t bann_num_precisions(const bann_ctx* ctx, int32_t b);
+
+/* BranchParams::from_host / load_param_vec (params.rs:634-698) */
+int bann_branch_set_params(bann_ctx* ctx, int32_t b, const float* param_vec);
+/* BranchParams::to_host / param_vec (params.rs:663-715) */
+int bann_branch_get_params(bann_ctx* ctx, int32_t b, float* param_vec_out);
+/* BranchPrecisions::from_host (params.rs:248-262) */
+int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float* precision_vec);
+int bann_branch_get_precisions(bann_ctx* ctx, int32_t b, float* precision_vec_out);
+/* target y_b (n floats) the branch is fitted to: the partial residual
+ * residual + f_b(theta) of net.rs:279-280 */
+int bann_branch_set_target(bann_ctx* ctx, int32_t b, const float* y);
+int bann_set_target_all(bann_ctx* ctx, const float* y);
+
+/* ---------------- per-branch math: replaces the BranchSampler methods ---------------- */
+/* predict (branch_sampler.rs:915-918, forward_feed 743-782): pred_out[n] */
+int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out);
+/* rss (branch_sampler.rs:905-909) against the branch target */
+int bann_rss(bann_ctx* ctx, int32_t b, double* rss_out);
+/* log_density_gradient (branch_sampler.rs:380-391: backpropagate 813-875 +
+ * the prior's log_density_gradient_wrt_weights, e.g. ridge_ard.rs:196-219, and
+ * log_density_gradient_wrt_biases 322-331); grad_out in param_vec order.
+ * rss_out (optional) receives the rss at the same parameters (823-828). */
+int bann_log_density_gradient(bann_ctx* ctx, int32_t b, float* grad_out, double* rss_out);
+/* log_density (branch_sampler.rs:72-78; std_normal_branch.rs:149-158) at the
+ * current parameters and the given rss */
+int bann_log_density(bann_ctx* ctx, int32_t b, double rss, double* out);
+/* neg_hamiltonian (branch_sampler.rs:878-883) with momentum p (param_vec order) */
+int bann_neg_hamiltonian(bann_ctx* ctx, int32_t b, const float* momentum, double* out);
+
+/* ---------------- HMC: replaces hmc_step (branch_sampler.rs:1192-1299) ----------------
+ * Runs one HMC trajectory of L leapfrog steps for each branch in
+ * branches[0..nb), all branches packed into one grad launch + one update
+ * launch per leapfrog step.  Branches are independent (each against its own
+ * target).  RNG draws may be injected for parity (SURVEY §0 caveat 3):
+ *   step_mode == BANN_STEP_INJECTED: eps = concatenated per-branch step-size
+ *       vectors (param_vec order); otherwise eps may be NULL and the sizes are
+ *       computed on the device (izmailov_step_sizes, ridge_ard.rs:70-117 etc.;
+ *       uniform 706-732) with factor step_factor.
+ *   momentum: concatenated p0 (param_vec order), or NULL to sample N(0,1) on
+ *       the device from seed.
+ *   u: one acceptance uniform per branch (branch_sampler.rs:546-548).
+ * Outputs (each may be NULL): status_out[nb] (bann_hmc_status),
+ * h_trace_out[nb*(L+1)] (-H after each step; entry 0 = initial; a branch that
+ * was rejected early stops updating its trace), uturn_out[nb] (first step with
+ * net_movement < 0, 551-592, or -1), log_density_out[nb] (accepted state).
+ * Rejected / early-rejected branches are restored to their initial params. */
+int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_hamiltonian_error,
+                  int32_t step_mode, float step_factor, const float* eps, const float* momentum, uint64_t seed,
+                  const float* u, int32_t* status_out, double* h_trace_out, int32_t* uturn_out,
+                  double* log_density_out);
+
+/* ---------------- benchmark / production leapfrog stepping ----------------
+ * Device-resident trajectory state for a fixed branch set: begin samples the
+ * momenta on the device and evaluates the initial gradient and -H; each
+ * leapfrog step is one packed gradient launch + one fused update launch with
+ * no host synchronisation; end performs the final half step, the Metropolis
+ * decision (uniforms from seed) and restores rejected branches. */
+int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_hamiltonian_error,
+                        int32_t step_mode, float step_factor, uint64_t seed);
+int bann_leapfrog_steps(bann_ctx* ctx, int32_t k);
+int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* num_accepted);
+/* device pointer to the branch predictions f_b(theta_L) written by the last
+ * leapfrog step (indexed by branch id: pred[b*n + i]), for the residual update. */
+int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out);
+int bann_synchronize(bann_ctx* ctx);
+
+/* ---------------- introspection for tests / profiling ---------------- */
+/* which gradient kernel serves branch b: 1 = fused single-pass MFMA/VALU kernel,
+ * 0 = generic multi-pass kernels */
+int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
+/* force every branch onto the generic path (0) or allow the fused path (1) */
+int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
+/* bytes of packed genotype data read per full gradient evaluation of all branches */
+int64_t bann_packed_genotype_bytes(const bann_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BANN_H */

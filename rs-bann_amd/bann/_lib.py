@@ -1,0 +1,99 @@
+"""ctypes binding of include/bann.h (librsbann_amd.so, built in-tree).
+
+The product path is the HIP library; there is no CPU fallback.  If the shared
+library is missing, importing the compute API raises ``BannLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)                       # rs-bann_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "librsbann_amd.so")
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "bann.h")
+
+BANN_OK = 0
+STATUS = {0: "BANN_OK", -1: "BANN_E_HIP", -2: "BANN_E_SHAPE", -3: "BANN_E_OOM", -4: "BANN_E_STATE",
+          -5: "BANN_E_ARG"}
+ACTIVATIONS = {"tanh": 0, "relu": 1, "leaky_relu": 2, "silu": 3, "identity": 4}
+PRIORS = {"ridge_ard": 0, "ridge_base": 1, "lasso_ard": 2, "lasso_base": 3, "std_normal": 4}
+STEP_MODES = {"uniform": 0, "random": 1, "izmailov": 3, "injected": 100}
+HMC_STATUS = {0: "accepted", 1: "rejected", 2: "rejected_early"}
+
+
+class BannLibraryError(RuntimeError):
+    pass
+
+
+class BannError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_P = C.c_void_p
+_i32, _i64, _u64, _f32, _f64 = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_double
+_pi8, _pu8 = C.POINTER(C.c_int8), C.POINTER(C.c_uint8)
+_pi32, _pf32, _pf64 = C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(C.c_double)
+
+# name -> (restype, argtypes); mirrors include/bann.h one to one
+SIGNATURES = {
+    "bann_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
+    "bann_ctx_destroy": (C.c_int, [_P]),
+    "bann_last_error": (C.c_char_p, [_P]),
+    "bann_version": (C.c_char_p, []),
+    "bann_genotypes_upload": (C.c_int, [_P, _pi8, _i64, _i64]),
+    "bann_genotypes_upload_bed": (C.c_int, [_P, _pu8, _i64, _i64]),
+    "bann_genotypes_synthetic": (C.c_int, [_P, _i64, _i64, _u64]),
+    "bann_genotypes_stats": (C.c_int, [_P, _pf32, _pf32]),
+    "bann_genotypes_set_stats": (C.c_int, [_P, _pf32, _pf32]),
+    "bann_genotypes_download": (C.c_int, [_P, _pi32, _i32, _pi8]),
+    "bann_branch_add": (C.c_int, [_P, _pi32, _i32, _pi32, _i32, _i32, _i32]),
+    "bann_finalize": (C.c_int, [_P, _i32]),
+    "bann_num_branches": (C.c_int, [_P]),
+    "bann_num_params": (_i64, [_P, _i32]),
+    "bann_num_precisions": (_i64, [_P, _i32]),
+    "bann_branch_set_params": (C.c_int, [_P, _i32, _pf32]),
+    "bann_branch_get_params": (C.c_int, [_P, _i32, _pf32]),
+    "bann_branch_set_precisions": (C.c_int, [_P, _i32, _pf32]),
+    "bann_branch_get_precisions": (C.c_int, [_P, _i32, _pf32]),
+    "bann_branch_set_target": (C.c_int, [_P, _i32, _pf32]),
+    "bann_set_target_all": (C.c_int, [_P, _pf32]),
+    "bann_predict": (C.c_int, [_P, _i32, _pf32]),
+    "bann_rss": (C.c_int, [_P, _i32, _pf64]),
+    "bann_log_density_gradient": (C.c_int, [_P, _i32, _pf32, _pf64]),
+    "bann_log_density": (C.c_int, [_P, _i32, _f64, _pf64]),
+    "bann_neg_hamiltonian": (C.c_int, [_P, _i32, _pf32, _pf64]),
+    "bann_hmc_step": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pi32, _pf64,
+                                _pi32, _pf64]),
+    "bann_leapfrog_begin": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _u64]),
+    "bann_leapfrog_steps": (C.c_int, [_P, _i32]),
+    "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),
+    "bann_leapfrog_predictions_device": (C.c_int, [_P, C.POINTER(_pf32)]),
+    "bann_synchronize": (C.c_int, [_P]),
+    "bann_branch_kernel_path": (C.c_int, [_P, _i32]),
+    "bann_set_fused_enabled": (C.c_int, [_P, _i32]),
+    "bann_packed_genotype_bytes": (_i64, [_P]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load librsbann_amd.so and attach the signatures.  Raises loudly if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise BannLibraryError(
+            f"{path} not found: build the HIP library first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or make -C rs-bann_amd/csrc).  There is no CPU fallback.")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

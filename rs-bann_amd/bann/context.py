@@ -1,0 +1,233 @@
+"""Pythonic host mirror of the C ABI (include/bann.h).
+
+``BannContext`` owns one device context.  Method names follow the reference's
+BranchSampler / BranchStruct vocabulary (src/net/branch/branch_sampler.rs):
+``predict``, ``rss``, ``log_density_gradient``, ``log_density``,
+``neg_hamiltonian``, ``hmc_step``.  Every call goes through the HIP library;
+nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ._lib import ACTIVATIONS, PRIORS, STEP_MODES, BannError, load_library
+
+
+def _ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+class BannContext:
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        rc = self._lib.bann_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise BannError(rc, f"bann_ctx_create(device={device}) failed (no HIP device?)")
+        self._h = h
+        self.n = 0
+        self.num_markers = 0
+        self._branches = []
+
+    # ------------------------------------------------------------------ util
+    def _check(self, rc):
+        if rc < 0:
+            raise BannError(rc, self._lib.bann_last_error(self._h).decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.bann_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------- genotypes
+    def upload_genotypes(self, g: np.ndarray):
+        """g: int8 [num_markers][n] variant-major (bed.rs layout)."""
+        g = np.ascontiguousarray(g, dtype=np.int8)
+        M, n = g.shape
+        self._check(self._lib.bann_genotypes_upload(self._h, _ptr(g, C.c_int8), n, M))
+        self.n, self.num_markers = n, M
+
+    def upload_bed(self, payload: bytes, n: int, num_markers: int):
+        buf = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+        self._check(self._lib.bann_genotypes_upload_bed(self._h, _ptr(buf, C.c_uint8), n, num_markers))
+        self.n, self.num_markers = n, num_markers
+
+    def synthetic_genotypes(self, n: int, num_markers: int, seed: int = 42):
+        self._check(self._lib.bann_genotypes_synthetic(self._h, n, num_markers, seed))
+        self.n, self.num_markers = n, num_markers
+
+    def genotype_stats(self):
+        mu = np.zeros(self.num_markers, np.float32)
+        sd = np.zeros(self.num_markers, np.float32)
+        self._check(self._lib.bann_genotypes_stats(self._h, _ptr(mu, C.c_float), _ptr(sd, C.c_float)))
+        return mu, sd
+
+    def set_genotype_stats(self, mu, sigma):
+        m = _f32(mu)
+        s = _f32(sigma)
+        self._check(self._lib.bann_genotypes_set_stats(self._h, _ptr(m, C.c_float), _ptr(s, C.c_float)))
+
+    def download_genotypes(self, snp_idx: Sequence[int]) -> np.ndarray:
+        idx = np.ascontiguousarray(snp_idx, dtype=np.int32)
+        out = np.zeros((idx.size, self.n), np.int8)
+        self._check(self._lib.bann_genotypes_download(self._h, _ptr(idx, C.c_int32), idx.size, _ptr(out, C.c_int8)))
+        return out
+
+    # -------------------------------------------------------------- branches
+    def add_branch(self, snp_idx: Sequence[int], layer_widths: Sequence[int], activation: str = "tanh",
+                   prior: str = "ridge_ard") -> int:
+        idx = np.ascontiguousarray(snp_idx, dtype=np.int32)
+        w = np.ascontiguousarray(layer_widths, dtype=np.int32)
+        b = self._check(self._lib.bann_branch_add(self._h, _ptr(idx, C.c_int32), idx.size, _ptr(w, C.c_int32), w.size,
+                                                  ACTIVATIONS[activation], PRIORS[prior]))
+        self._branches.append((idx.copy(), list(layer_widths), activation, prior))
+        return b
+
+    def set_fused_enabled(self, enabled: bool):
+        self._check(self._lib.bann_set_fused_enabled(self._h, 1 if enabled else 0))
+
+    def finalize(self, free_raw: bool = False):
+        self._check(self._lib.bann_finalize(self._h, 1 if free_raw else 0))
+
+    @property
+    def num_branches(self) -> int:
+        return self._check(self._lib.bann_num_branches(self._h))
+
+    def num_params(self, b: int) -> int:
+        return int(self._check(self._lib.bann_num_params(self._h, b)))
+
+    def num_precisions(self, b: int) -> int:
+        return int(self._check(self._lib.bann_num_precisions(self._h, b)))
+
+    def kernel_path(self, b: int) -> str:
+        return "fused" if self._check(self._lib.bann_branch_kernel_path(self._h, b)) == 1 else "generic"
+
+    @property
+    def packed_genotype_bytes(self) -> int:
+        return int(self._lib.bann_packed_genotype_bytes(self._h))
+
+    def set_params(self, b: int, param_vec):
+        v = _f32(param_vec)
+        assert v.size == self.num_params(b), "param_vec size"
+        self._check(self._lib.bann_branch_set_params(self._h, b, _ptr(v, C.c_float)))
+
+    def get_params(self, b: int) -> np.ndarray:
+        out = np.zeros(self.num_params(b), np.float32)
+        self._check(self._lib.bann_branch_get_params(self._h, b, _ptr(out, C.c_float)))
+        return out
+
+    def set_precisions(self, b: int, precision_vec):
+        v = _f32(precision_vec)
+        assert v.size == self.num_precisions(b), "precision_vec size"
+        self._check(self._lib.bann_branch_set_precisions(self._h, b, _ptr(v, C.c_float)))
+
+    def get_precisions(self, b: int) -> np.ndarray:
+        out = np.zeros(self.num_precisions(b), np.float32)
+        self._check(self._lib.bann_branch_get_precisions(self._h, b, _ptr(out, C.c_float)))
+        return out
+
+    def set_target(self, b: int, y):
+        v = _f32(y)
+        assert v.size == self.n
+        self._check(self._lib.bann_branch_set_target(self._h, b, _ptr(v, C.c_float)))
+
+    def set_target_all(self, y):
+        v = _f32(y)
+        assert v.size == self.n
+        self._check(self._lib.bann_set_target_all(self._h, _ptr(v, C.c_float)))
+
+    # ------------------------------------------------------- branch sampler
+    def predict(self, b: int) -> np.ndarray:
+        out = np.zeros(self.n, np.float32)
+        self._check(self._lib.bann_predict(self._h, b, _ptr(out, C.c_float)))
+        return out
+
+    def rss(self, b: int) -> float:
+        r = C.c_double()
+        self._check(self._lib.bann_rss(self._h, b, C.byref(r)))
+        return r.value
+
+    def log_density_gradient(self, b: int):
+        g = np.zeros(self.num_params(b), np.float32)
+        r = C.c_double()
+        self._check(self._lib.bann_log_density_gradient(self._h, b, _ptr(g, C.c_float), C.byref(r)))
+        return g, r.value
+
+    def log_density(self, b: int, rss: float) -> float:
+        out = C.c_double()
+        self._check(self._lib.bann_log_density(self._h, b, float(rss), C.byref(out)))
+        return out.value
+
+    def neg_hamiltonian(self, b: int, momentum) -> float:
+        p = _f32(momentum)
+        out = C.c_double()
+        self._check(self._lib.bann_neg_hamiltonian(self._h, b, _ptr(p, C.c_float), C.byref(out)))
+        return out.value
+
+    def hmc_step(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,
+                 step_mode: str = "izmailov", step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0,
+                 u=None):
+        """One HMC trajectory per branch, all branches packed (branch_sampler.rs:1192-1299)."""
+        br = np.ascontiguousarray(branches, dtype=np.int32)
+        nb = br.size
+        eps_a = _f32(eps) if eps is not None else None
+        mom_a = _f32(momentum) if momentum is not None else None
+        u_a = _f32(u) if u is not None else None
+        status = np.zeros(nb, np.int32)
+        trace = np.zeros((nb, L + 1), np.float64)
+        uturn = np.zeros(nb, np.int32)
+        ld = np.zeros(nb, np.float64)
+        mode = STEP_MODES["injected"] if eps is not None else STEP_MODES[step_mode]
+        nullf = C.POINTER(C.c_float)()
+        self._check(self._lib.bann_hmc_step(
+            self._h, _ptr(br, C.c_int32), nb, L, max_hamiltonian_error, mode, step_factor,
+            _ptr(eps_a, C.c_float) if eps_a is not None else nullf,
+            _ptr(mom_a, C.c_float) if mom_a is not None else nullf, seed,
+            _ptr(u_a, C.c_float) if u_a is not None else nullf,
+            _ptr(status, C.c_int32), _ptr(trace, C.c_double), _ptr(uturn, C.c_int32), _ptr(ld, C.c_double)))
+        return dict(status=status, trace=trace, uturn=uturn, log_density=ld)
+
+    # ------------------------------------------------------ leapfrog session
+    def leapfrog_begin(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,
+                       step_mode: str = "izmailov", step_factor: float = 1.0, seed: int = 0):
+        br = np.ascontiguousarray(branches, dtype=np.int32)
+        self._lf_nb = br.size
+        self._check(self._lib.bann_leapfrog_begin(self._h, _ptr(br, C.c_int32), br.size, L, max_hamiltonian_error,
+                                                  STEP_MODES[step_mode], step_factor, seed))
+
+    def leapfrog_steps(self, k: int):
+        self._check(self._lib.bann_leapfrog_steps(self._h, k))
+
+    def leapfrog_end(self):
+        st = np.zeros(self._lf_nb, np.int32)
+        acc = C.c_int32()
+        self._check(self._lib.bann_leapfrog_end(self._h, _ptr(st, C.c_int32), C.byref(acc)))
+        return st, acc.value
+
+    def predictions_device_ptr(self) -> int:
+        p = C.POINTER(C.c_float)()
+        self._check(self._lib.bann_leapfrog_predictions_device(self._h, C.byref(p)))
+        return C.cast(p, C.c_void_p).value or 0
+
+    def synchronize(self):
+        self._check(self._lib.bann_synchronize(self._h))

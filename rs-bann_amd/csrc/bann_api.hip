@@ -1,0 +1,947 @@
+// bann_api.hip — C ABI of include/bann.h: context, genotype ingestion, branch
+// registry, per-branch BranchSampler math, and the packed HMC driver.
+//
+// Host-side counterpart of the reference's per-branch orchestration:
+//   B::from_cfg / to_cfg          branch_struct.rs:12-29, branch_sampler.rs:155-171
+//   hmc_step                       branch_sampler.rs:1192-1299
+//   izmailov / uniform / random step sizes (ridge_ard.rs:70-117, ...)
+// The device work is in kernels_{data,grad,update}.hip.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/bann.h"
+#include "bann_internal.h"
+
+#define BANN_VERSION "rs-bann_amd 0.1.0 (gfx950, HIP)"
+
+namespace {
+
+struct BranchHost {
+  std::vector<int32_t> snp_idx;
+  std::vector<int32_t> widths;
+  int32_t m = 0, L = 0, act = 0, prior = 0;
+  int32_t P = 0, nprec = 0;
+  std::vector<float> prec;  // precision_vec order
+  BranchDev dev{};
+};
+
+struct Plan {
+  std::vector<int32_t> all, generic;
+  std::vector<GradItem> items[5];
+  int32_t nwaves[5] = {0, 0, 0, 0, 0};
+  int32_t max_p_generic = 0, max_p = 0;
+  int32_t* d_all = nullptr;
+  int32_t* d_gen = nullptr;
+  GradItem* d_items[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool owns = false;
+};
+
+}  // namespace
+
+struct bann_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // genotypes
+  int64_t n = 0, M = 0;
+  int8_t* d_g = nullptr;
+  float* d_mu = nullptr;
+  float* d_sigma = nullptr;
+  // branches
+  std::vector<BranchHost> br;
+  bool finalized = false;
+  bool fused_enabled = true;
+  int32_t nfrag = 0, max_splits = 1;
+  int64_t packed_bytes = 0, total_p = 0;
+  // device buffers
+  BranchDev* d_br = nullptr;
+  int8_t* d_xpk = nullptr;
+  uint8_t* d_dig = nullptr;
+  FusedConst* d_fc = nullptr;
+  float *d_mub = nullptr, *d_sigb = nullptr;
+  float *d_theta = nullptr, *d_mom = nullptr, *d_eps = nullptr, *d_theta0 = nullptr, *d_lam = nullptr,
+        *d_lamld = nullptr, *d_grad = nullptr, *d_part = nullptr;
+  double* d_rss_part = nullptr;
+  float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
+  double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
+  int32_t *d_status = nullptr, *d_uturn = nullptr;
+  int32_t htrace_cap = 0;  // L+1 capacity of d_htrace rows
+  // scratch plan buffers (per-call plans)
+  int32_t* d_list_scr = nullptr;
+  int32_t* d_gen_scr = nullptr;
+  GradItem* d_items_scr = nullptr;
+  int64_t items_cap = 0;
+  // leapfrog session
+  Plan lf;
+  bool lf_active = false;
+  int32_t lf_L = 0, lf_step = 0;
+  DevState st{};
+};
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+static int fail(bann_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define CK(call)                                                                          \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(ctx, e_ == hipErrorOutOfMemory ? BANN_E_OOM : BANN_E_HIP,              \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+template <typename T>
+static hipError_t dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) count = 1;
+  return hipMalloc((void**)p, (size_t)count * sizeof(T));
+}
+
+static void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+static void free_plan(Plan& p) {
+  if (p.owns) {
+    dfree(p.d_all);
+    dfree(p.d_gen);
+    for (auto& d : p.d_items) dfree(d);
+  }
+  p = Plan{};
+}
+
+static void refresh_state(bann_ctx* ctx) {
+  DevState& s = ctx->st;
+  s.br = ctx->d_br;
+  s.xpk = ctx->d_xpk;
+  s.dig = ctx->d_dig;
+  s.fc = ctx->d_fc;
+  s.mu = ctx->d_mub;
+  s.sigma = ctx->d_sigb;
+  s.theta = ctx->d_theta;
+  s.mom = ctx->d_mom;
+  s.eps = ctx->d_eps;
+  s.theta0 = ctx->d_theta0;
+  s.lam = ctx->d_lam;
+  s.lamld = ctx->d_lamld;
+  s.grad = ctx->d_grad;
+  s.part = ctx->d_part;
+  s.rss_part = ctx->d_rss_part;
+  s.y = ctx->d_y;
+  s.pred = ctx->d_pred;
+  s.scr = ctx->d_scr;
+  s.eprec = ctx->d_eprec;
+  s.h0 = ctx->d_h0;
+  s.htrace = ctx->d_htrace;
+  s.ld_out = ctx->d_ld;
+  s.rss_out = ctx->d_rss;
+  s.status = ctx->d_status;
+  s.uturn = ctx->d_uturn;
+  s.uacc = ctx->d_u;
+  s.n = ctx->n;
+  s.nfrag = ctx->nfrag;
+  s.max_splits = ctx->max_splits;
+  s.lint = ctx->htrace_cap - 1;
+}
+
+static bool check_branch(const bann_ctx* ctx, int32_t b) {
+  return ctx && ctx->finalized && b >= 0 && b < (int32_t)ctx->br.size();
+}
+
+// expanded per-parameter precision multipliers and the error precision
+static void expand_precisions(const BranchHost& h, std::vector<float>& lam, std::vector<float>& lamld,
+                              float& eprec) {
+  const BranchDev& d = h.dev;
+  lam.assign(h.P, 0.f);
+  lamld.assign(h.P, 0.f);
+  const bool ard = (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD);
+  int pi = 0;
+  for (int l = 0; l < h.L; ++l) {
+    const int wi = d.win[l], wo = d.widths[l];
+    for (int k = 0; k < wo; ++k)
+      for (int j = 0; j < wi; ++j) {
+        float v;
+        if (h.prior == BANN_STD_NORMAL)
+          v = 1.f;
+        else if (ard && l < h.L - 1)
+          v = h.prec[pi + j];
+        else
+          v = h.prec[pi];
+        lam[d.woff[l] + k * wi + j] = v;
+        lamld[d.woff[l] + k * wi + j] = v;
+      }
+    pi += (ard && l < h.L - 1) ? wi : 1;
+  }
+  if (h.prior == BANN_STD_NORMAL)  // std_normal_branch.rs:149-158: l2 bias term in log_density only
+    for (int l = 0; l < h.L - 1; ++l)
+      for (int k = 0; k < d.widths[l]; ++k) lamld[d.boff[l] + k] = 1.f;
+  eprec = h.prec.back();
+}
+
+// step sizes in param_vec order (izmailov_step_sizes ridge_ard.rs:70-117, ridge_base.rs:83-114,
+// lasso_ard.rs:77-117, lasso_base.rs:83-114, std_normal_branch.rs:83-114; uniform 706-732;
+// random 654-681)
+static void host_step_sizes(const BranchHost& h, int mode, float c, int lint, std::mt19937_64& rng,
+                            std::vector<float>& eps) {
+  const BranchDev& d = h.dev;
+  eps.assign(h.P, c);
+  if (mode == BANN_STEP_UNIFORM) return;
+  if (mode == BANN_STEP_RANDOM) {
+    std::uniform_real_distribution<float> U(0.f, 1.f);
+    const float f = powf((float)h.P, -0.25f) * c;
+    for (auto& e : eps) e = U(rng) * f;
+    return;
+  }
+  const bool ard = (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD);
+  const bool lasso = (h.prior == BANN_LASSO_ARD || h.prior == BANN_LASSO_BASE);
+  const double PI = 3.14159265358979323846;
+  int pi = 0;
+  for (int l = 0; l < h.L; ++l) {
+    const int wi = d.win[l], wo = d.widths[l];
+    for (int k = 0; k < wo; ++k)
+      for (int j = 0; j < wi; ++j) {
+        const double lam = (ard && l < h.L - 1) ? h.prec[pi + j] : h.prec[pi];
+        double e;
+        if (h.prior == BANN_STD_NORMAL)
+          e = PI / (2.0 * sqrt(lam) * lint);
+        else if (lasso)
+          e = c / (4.0 * lam * lint);
+        else
+          e = c * PI / (2.0 * sqrt(lam) * lint);
+        eps[d.woff[l] + k * wi + j] = (float)e;
+      }
+    pi += (ard && l < h.L - 1) ? wi : 1;
+  }
+  for (int l = 0; l < h.L - 1; ++l) {
+    const double lb = h.prec[pi + l];
+    const double cc = h.prior == BANN_STD_NORMAL ? 1.0 : c;
+    for (int k = 0; k < d.widths[l]; ++k) eps[d.boff[l] + k] = (float)(cc * PI / (2.0 * sqrt(lb) * lint));
+  }
+}
+
+static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent) {
+  free_plan(p);
+  p.all.assign(branches, branches + nb);
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
+    if (b < 0 || b >= (int32_t)ctx->br.size()) return fail(ctx, BANN_E_SHAPE, "branch index out of range");
+    const BranchHost& h = ctx->br[b];
+    p.max_p = std::max(p.max_p, h.P);
+    if (!h.dev.fused) {
+      p.generic.push_back(b);
+      p.max_p_generic = std::max(p.max_p_generic, h.P);
+      continue;
+    }
+    const int L = h.L;
+    const int64_t nfrag = ctx->nfrag;
+    const int ns = h.dev.nsplits;
+    for (int s = 0; s < ns; ++s) {
+      GradItem it;
+      it.branch = b;
+      it.split = s;
+      it.frag_begin = (int32_t)(nfrag * s / ns);
+      it.frag_end = (int32_t)(nfrag * (s + 1) / ns);
+      p.items[L].push_back(it);
+    }
+    p.nwaves[L] = std::max(p.nwaves[L], h.dev.nchunks);
+  }
+  if (persistent) {
+    p.owns = true;
+    CK(dalloc(&p.d_all, nb));
+    CK(dalloc(&p.d_gen, (int64_t)p.generic.size()));
+    CK(hipMemcpyAsync(p.d_all, p.all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    if (!p.generic.empty())
+      CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                        ctx->stream));
+    for (int L = 2; L <= 4; ++L) {
+      if (p.items[L].empty()) continue;
+      CK(dalloc(&p.d_items[L], (int64_t)p.items[L].size()));
+      CK(hipMemcpyAsync(p.d_items[L], p.items[L].data(), p.items[L].size() * sizeof(GradItem),
+                        hipMemcpyHostToDevice, ctx->stream));
+    }
+  } else {
+    p.owns = false;
+    p.d_all = ctx->d_list_scr;
+    p.d_gen = ctx->d_gen_scr;
+    CK(hipMemcpyAsync(p.d_all, p.all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    if (!p.generic.empty())
+      CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                        ctx->stream));
+    int64_t off = 0;
+    for (int L = 2; L <= 4; ++L) {
+      if (p.items[L].empty()) continue;
+      p.d_items[L] = ctx->d_items_scr + off;
+      CK(hipMemcpyAsync(p.d_items[L], p.items[L].data(), p.items[L].size() * sizeof(GradItem),
+                        hipMemcpyHostToDevice, ctx->stream));
+      off += (int64_t)p.items[L].size();
+    }
+  }
+  return BANN_OK;
+}
+
+// gradient (partials) of every branch in the plan at the current theta
+static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
+  for (int L = 2; L <= 4; ++L)
+    if (!p.items[L].empty())
+      launch_fused_grad(ctx->st, p.d_items[L], (int32_t)p.items[L].size(), p.nwaves[L], L, write_pred,
+                        ctx->stream);
+  if (!p.generic.empty())
+    launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
+  CK(hipGetLastError());
+  return BANN_OK;
+}
+
+static int ensure_htrace(bann_ctx* ctx, int32_t L) {
+  if (L + 1 <= ctx->htrace_cap) return BANN_OK;
+  dfree(ctx->d_htrace);
+  ctx->d_htrace = nullptr;
+  CK(dalloc(&ctx->d_htrace, (int64_t)ctx->br.size() * (L + 1)));
+  ctx->htrace_cap = L + 1;
+  refresh_state(ctx);
+  return BANN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+extern "C" const char* bann_version(void) { return BANN_VERSION; }
+
+extern "C" int bann_ctx_create(int device, bann_ctx** out) {
+  if (!out) return BANN_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return BANN_E_HIP;
+  if (device < 0 || device >= ndev) return BANN_E_ARG;
+  bann_ctx* ctx = new bann_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return BANN_E_HIP;
+  }
+  *out = ctx;
+  return BANN_OK;
+}
+
+extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
+  if (!ctx) return BANN_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  free_plan(ctx->lf);
+  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_dig, ctx->d_fc, ctx->d_mub,
+                  ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
+                  ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_scr, ctx->d_eprec,
+                  ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
+                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr};
+  for (void* p : bufs) dfree(p);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return BANN_OK;
+}
+
+extern "C" const char* bann_last_error(const bann_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+extern "C" int bann_synchronize(bann_ctx* ctx) {
+  if (!ctx) return BANN_E_ARG;
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// genotypes
+// ---------------------------------------------------------------------------
+static int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M) {
+  if (ctx->finalized) return fail(ctx, BANN_E_STATE, "genotypes must be set before bann_finalize");
+  if (n <= 0 || M <= 0) return fail(ctx, BANN_E_SHAPE, "n and num_markers must be positive");
+  CK(hipSetDevice(ctx->device));
+  dfree(ctx->d_g);
+  dfree(ctx->d_mu);
+  dfree(ctx->d_sigma);
+  ctx->d_g = nullptr;
+  ctx->d_mu = ctx->d_sigma = nullptr;
+  ctx->n = n;
+  ctx->M = M;
+  CK(dalloc(&ctx->d_g, n * M));
+  CK(dalloc(&ctx->d_mu, M));
+  CK(dalloc(&ctx->d_sigma, M));
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_upload(bann_ctx* ctx, const int8_t* g, int64_t n, int64_t num_markers) {
+  if (!ctx || !g) return BANN_E_ARG;
+  int rc = alloc_genotypes(ctx, n, num_markers);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(ctx->d_g, g, (size_t)(n * num_markers), hipMemcpyHostToDevice, ctx->stream));
+  launch_col_stats(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_upload_bed(bann_ctx* ctx, const uint8_t* payload, int64_t n, int64_t num_markers) {
+  if (!ctx || !payload) return BANN_E_ARG;
+  int rc = alloc_genotypes(ctx, n, num_markers);
+  if (rc) return rc;
+  const int64_t bytes = ((n + 3) / 4) * num_markers;
+  uint8_t* d_pl = nullptr;
+  CK(dalloc(&d_pl, bytes));
+  CK(hipMemcpyAsync(d_pl, payload, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+  launch_decode_bed(d_pl, ctx->d_g, n, num_markers, ctx->stream);
+  launch_col_stats(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  dfree(d_pl);
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_synthetic(bann_ctx* ctx, int64_t n, int64_t num_markers, uint64_t seed) {
+  if (!ctx) return BANN_E_ARG;
+  int rc = alloc_genotypes(ctx, n, num_markers);
+  if (rc) return rc;
+  launch_synthetic_genotypes(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, seed, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_stats(bann_ctx* ctx, float* mu, float* sigma) {
+  if (!ctx || !ctx->d_mu) return fail(ctx, BANN_E_STATE, "no genotypes");
+  if (mu) CK(hipMemcpy(mu, ctx->d_mu, ctx->M * sizeof(float), hipMemcpyDeviceToHost));
+  if (sigma) CK(hipMemcpy(sigma, ctx->d_sigma, ctx->M * sizeof(float), hipMemcpyDeviceToHost));
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_set_stats(bann_ctx* ctx, const float* mu, const float* sigma) {
+  if (!ctx || !mu || !sigma) return BANN_E_ARG;
+  if (!ctx->d_mu) return fail(ctx, BANN_E_STATE, "no genotypes");
+  if (ctx->finalized) return fail(ctx, BANN_E_STATE, "statistics are folded at bann_finalize; set them before");
+  CK(hipMemcpy(ctx->d_mu, mu, ctx->M * sizeof(float), hipMemcpyHostToDevice));
+  CK(hipMemcpy(ctx->d_sigma, sigma, ctx->M * sizeof(float), hipMemcpyHostToDevice));
+  return BANN_OK;
+}
+
+extern "C" int bann_genotypes_download(bann_ctx* ctx, const int32_t* snp_idx, int32_t m, int8_t* g_out) {
+  if (!ctx || !snp_idx || !g_out || m <= 0) return BANN_E_ARG;
+  if (!ctx->d_g) return fail(ctx, BANN_E_STATE, "raw genotypes not resident (freed at finalize?)");
+  for (int i = 0; i < m; ++i)
+    if (snp_idx[i] < 0 || snp_idx[i] >= ctx->M) return fail(ctx, BANN_E_SHAPE, "marker index out of range");
+  int32_t* d_idx = nullptr;
+  int8_t* d_out = nullptr;
+  CK(dalloc(&d_idx, m));
+  CK(dalloc(&d_out, (int64_t)m * ctx->n));
+  CK(hipMemcpyAsync(d_idx, snp_idx, m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  launch_unpack_markers(ctx->d_g, d_idx, m, ctx->n, d_out, ctx->stream);
+  CK(hipMemcpyAsync(g_out, d_out, (size_t)m * ctx->n, hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  dfree(d_idx);
+  dfree(d_out);
+  return BANN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// branches
+// ---------------------------------------------------------------------------
+extern "C" int bann_branch_add(bann_ctx* ctx, const int32_t* snp_idx, int32_t m, const int32_t* layer_widths,
+                               int32_t num_layers, int32_t activation, int32_t prior) {
+  if (!ctx || !snp_idx || !layer_widths) return BANN_E_ARG;
+  if (ctx->finalized) return fail(ctx, BANN_E_STATE, "branch set is fixed after bann_finalize");
+  if (m <= 0) return fail(ctx, BANN_E_SHAPE, "a branch needs at least one marker");
+  if (num_layers < 2 || num_layers > BANN_MAXL)
+    return fail(ctx, BANN_E_SHAPE, "num_layers must be in [2, 8] (summary + output at least)");
+  if (layer_widths[num_layers - 1] != 1) return fail(ctx, BANN_E_SHAPE, "output layer width must be 1");
+  if (activation < 0 || activation > 4) return fail(ctx, BANN_E_ARG, "unknown activation");
+  if (prior < 0 || prior > 4) return fail(ctx, BANN_E_ARG, "unknown prior");
+  BranchHost h;
+  h.snp_idx.assign(snp_idx, snp_idx + m);
+  h.widths.assign(layer_widths, layer_widths + num_layers);
+  for (int l = 0; l < num_layers; ++l)
+    if (h.widths[l] <= 0) return fail(ctx, BANN_E_SHAPE, "layer widths must be positive");
+  for (int i = 0; i < m; ++i)
+    if (snp_idx[i] < 0 || (ctx->M > 0 && snp_idx[i] >= ctx->M))
+      return fail(ctx, BANN_E_SHAPE, "marker index out of range");
+  h.m = m;
+  h.L = num_layers;
+  h.act = activation;
+  h.prior = prior;
+  BranchDev& d = h.dev;
+  d.m = m;
+  d.L = num_layers;
+  d.act = activation;
+  d.prior = prior;
+  int off = 0;
+  for (int l = 0; l < num_layers; ++l) {
+    d.widths[l] = h.widths[l];
+    d.win[l] = l == 0 ? m : h.widths[l - 1];
+    d.woff[l] = off;
+    off += d.win[l] * d.widths[l];
+  }
+  for (int l = 0; l < num_layers - 1; ++l) {
+    d.boff[l] = off;
+    off += d.widths[l];
+  }
+  d.P = h.P = off;
+  const bool ard = (prior == BANN_RIDGE_ARD || prior == BANN_LASSO_ARD);
+  int np = 0;
+  for (int l = 0; l < num_layers; ++l) np += (ard && l < num_layers - 1) ? d.win[l] : 1;
+  h.nprec = np + (num_layers - 1) + 1;
+  h.prec.assign(h.nprec, 1.f);
+  ctx->br.push_back(std::move(h));
+  return (int)ctx->br.size() - 1;
+}
+
+extern "C" int bann_num_branches(const bann_ctx* ctx) { return ctx ? (int)ctx->br.size() : BANN_E_ARG; }
+extern "C" int64_t bann_num_params(const bann_ctx* ctx, int32_t b) {
+  if (!ctx || b < 0 || b >= (int32_t)ctx->br.size()) return BANN_E_ARG;
+  return ctx->br[b].P;
+}
+extern "C" int64_t bann_num_precisions(const bann_ctx* ctx, int32_t b) {
+  if (!ctx || b < 0 || b >= (int32_t)ctx->br.size()) return BANN_E_ARG;
+  return ctx->br[b].nprec;
+}
+extern "C" int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b) {
+  if (!check_branch(ctx, b)) return BANN_E_ARG;
+  return ctx->br[b].dev.fused;
+}
+extern "C" int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled) {
+  if (!ctx) return BANN_E_ARG;
+  if (ctx->finalized) return fail(ctx, BANN_E_STATE, "set before bann_finalize");
+  ctx->fused_enabled = enabled != 0;
+  return BANN_OK;
+}
+extern "C" int64_t bann_packed_genotype_bytes(const bann_ctx* ctx) { return ctx ? ctx->packed_bytes : 0; }
+
+extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
+  if (!ctx) return BANN_E_ARG;
+  if (ctx->finalized) return fail(ctx, BANN_E_STATE, "already finalized");
+  if (!ctx->d_g) return fail(ctx, BANN_E_STATE, "no genotypes uploaded");
+  if (ctx->br.empty()) return fail(ctx, BANN_E_STATE, "no branches");
+  CK(hipSetDevice(ctx->device));
+  const int64_t n = ctx->n;
+  ctx->nfrag = (int32_t)((n + 15) / 16);
+  const int64_t npad = (int64_t)ctx->nfrag * 16;
+  // row splits of the fused kernel: ~target work items over all branches
+  int64_t total_frags = 0;
+  for (auto& h : ctx->br) {
+    for (int i = 0; i < h.m; ++i)
+      if (h.snp_idx[i] >= ctx->M) return fail(ctx, BANN_E_SHAPE, "marker index out of range");
+    BranchDev& d = h.dev;
+    d.nchunks = (h.m + BANN_CHUNK - 1) / BANN_CHUNK;
+    bool ok = ctx->fused_enabled && h.L >= 2 && h.L <= 4 && d.nchunks <= BANN_FUSED_MAXCH;
+    for (int l = 0; l < h.L; ++l) ok = ok && h.widths[l] <= BANN_FUSED_MAXW;
+    d.fused = ok ? 1 : 0;
+    if (d.fused) total_frags += ctx->nfrag;
+  }
+  int64_t target_items = 8192;
+  if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
+  const int64_t frags_per_item = std::max<int64_t>(8, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
+  int64_t x_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
+  int32_t max_splits = 1;
+  for (size_t b = 0; b < ctx->br.size(); ++b) {
+    BranchHost& h = ctx->br[b];
+    BranchDev& d = h.dev;
+    d.x_off = x_off;
+    x_off += (int64_t)ctx->nfrag * d.nchunks * 1024;
+    d.dig_off = dig_off;
+    if (d.fused) dig_off += (int64_t)d.nchunks * 1024;
+    d.p_off = p_off;
+    p_off += h.P;
+    d.mk_off = mk_off;
+    mk_off += h.m;
+    d.y_off = (int64_t)b * n;
+    d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
+    d.nsplits = std::min<int32_t>(d.nsplits, ctx->nfrag);
+    max_splits = std::max(max_splits, d.nsplits);
+    d.part_off = part_off;
+    part_off += (int64_t)d.nsplits * h.P;
+    if (d.fused) items += d.nsplits;
+    d.scr_off = scr_off;
+    if (!d.fused) {
+      int64_t o = 0;
+      for (int l = 0; l < h.L - 1; ++l) {
+        d.scr_z[l] = (int32_t)o;
+        o += npad * d.widths[l];
+        d.scr_a[l] = (int32_t)o;
+        o += npad * d.widths[l];
+        d.scr_d[l] = (int32_t)o;
+        o += npad * d.widths[l];
+      }
+      d.scr_d[h.L - 1] = (int32_t)o;
+      o += npad;
+      if (o >= (1ll << 31)) return fail(ctx, BANN_E_SHAPE, "generic-path scratch too large for one branch");
+      scr_off += o;
+    }
+  }
+  ctx->max_splits = max_splits;
+  ctx->packed_bytes = x_off;
+  ctx->total_p = p_off;
+  const int64_t nb = (int64_t)ctx->br.size();
+  CK(dalloc(&ctx->d_xpk, x_off));
+  CK(dalloc(&ctx->d_dig, dig_off));
+  CK(hipMemsetAsync(ctx->d_dig, 0, (size_t)std::max<int64_t>(dig_off, 1), ctx->stream));
+  CK(dalloc(&ctx->d_fc, nb));
+  CK(hipMemsetAsync(ctx->d_fc, 0, nb * sizeof(FusedConst), ctx->stream));
+  CK(dalloc(&ctx->d_mub, mk_off));
+  CK(dalloc(&ctx->d_sigb, mk_off));
+  float** pbufs[] = {&ctx->d_theta, &ctx->d_mom, &ctx->d_eps, &ctx->d_theta0, &ctx->d_lam, &ctx->d_lamld,
+                     &ctx->d_grad};
+  for (float** pb : pbufs) {
+    CK(dalloc(pb, p_off));
+    CK(hipMemsetAsync(*pb, 0, p_off * sizeof(float), ctx->stream));
+  }
+  CK(dalloc(&ctx->d_part, part_off));
+  CK(hipMemsetAsync(ctx->d_part, 0, part_off * sizeof(float), ctx->stream));
+  CK(dalloc(&ctx->d_rss_part, nb * max_splits));
+  CK(hipMemsetAsync(ctx->d_rss_part, 0, nb * max_splits * sizeof(double), ctx->stream));
+  CK(dalloc(&ctx->d_y, nb * n));
+  CK(hipMemsetAsync(ctx->d_y, 0, nb * n * sizeof(float), ctx->stream));
+  CK(dalloc(&ctx->d_pred, nb * n));
+  CK(hipMemsetAsync(ctx->d_pred, 0, nb * n * sizeof(float), ctx->stream));
+  CK(dalloc(&ctx->d_scr, scr_off));
+  CK(dalloc(&ctx->d_eprec, nb));
+  CK(dalloc(&ctx->d_u, nb));
+  CK(dalloc(&ctx->d_h0, nb));
+  CK(dalloc(&ctx->d_ld, nb));
+  CK(dalloc(&ctx->d_rss, nb));
+  CK(dalloc(&ctx->d_status, nb));
+  CK(dalloc(&ctx->d_uturn, nb));
+  CK(dalloc(&ctx->d_list_scr, nb));
+  CK(dalloc(&ctx->d_gen_scr, nb));
+  CK(dalloc(&ctx->d_items_scr, items));
+  ctx->items_cap = items;
+  // pack genotypes and gather marker statistics per branch
+  int32_t* d_idx = nullptr;
+  int32_t maxm = 0;
+  for (auto& h : ctx->br) maxm = std::max(maxm, h.m);
+  CK(dalloc(&d_idx, maxm));
+  std::vector<BranchDev> descs;
+  std::vector<float> lam, lamld, eprec(nb, 1.f);
+  for (size_t b = 0; b < ctx->br.size(); ++b) {
+    BranchHost& h = ctx->br[b];
+    CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    launch_pack_branch(ctx->d_g, d_idx, h.m, n, ctx->d_xpk + h.dev.x_off, h.dev.nchunks, ctx->nfrag, ctx->stream);
+    launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, h.m, ctx->d_mub + h.dev.mk_off, ctx->d_sigb + h.dev.mk_off,
+                        ctx->stream);
+    CK(hipGetLastError());
+    CK(hipStreamSynchronize(ctx->stream));  // d_idx reused
+    descs.push_back(h.dev);
+    float ep = 1.f;
+    expand_precisions(h, lam, lamld, ep);
+    eprec[b] = ep;
+    CK(hipMemcpyAsync(ctx->d_lam + h.dev.p_off, lam.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
+                      ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
+                      ctx->stream));
+  }
+  dfree(d_idx);
+  CK(dalloc(&ctx->d_br, nb));
+  CK(hipMemcpyAsync(ctx->d_br, descs.data(), nb * sizeof(BranchDev), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_eprec, eprec.data(), nb * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  ctx->finalized = true;
+  int rc = ensure_htrace(ctx, 1);
+  if (rc) return rc;
+  refresh_state(ctx);
+  CK(hipStreamSynchronize(ctx->stream));
+  if (free_raw) {
+    dfree(ctx->d_g);
+    ctx->d_g = nullptr;
+  }
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_set_params(bann_ctx* ctx, int32_t b, const float* param_vec) {
+  if (!check_branch(ctx, b) || !param_vec) return fail(ctx, BANN_E_ARG, "bad branch or null params");
+  const BranchHost& h = ctx->br[b];
+  CK(hipMemcpyAsync(ctx->d_theta + h.dev.p_off, param_vec, h.P * sizeof(float), hipMemcpyHostToDevice,
+                    ctx->stream));
+  int32_t bb = b;
+  CK(hipMemcpyAsync(ctx->d_list_scr, &bb, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  launch_fused_const(ctx->st, ctx->d_list_scr, 1, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_get_params(bann_ctx* ctx, int32_t b, float* out) {
+  if (!check_branch(ctx, b) || !out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  const BranchHost& h = ctx->br[b];
+  CK(hipMemcpyAsync(out, ctx->d_theta + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float* prec) {
+  if (!check_branch(ctx, b) || !prec) return fail(ctx, BANN_E_ARG, "bad branch or null precisions");
+  BranchHost& h = ctx->br[b];
+  h.prec.assign(prec, prec + h.nprec);
+  std::vector<float> lam, lamld;
+  float ep = 1.f;
+  expand_precisions(h, lam, lamld, ep);
+  CK(hipMemcpyAsync(ctx->d_lam + h.dev.p_off, lam.data(), h.P * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
+                    ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_eprec + b, &ep, sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_get_precisions(bann_ctx* ctx, int32_t b, float* out) {
+  if (!check_branch(ctx, b) || !out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  std::copy(ctx->br[b].prec.begin(), ctx->br[b].prec.end(), out);
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_set_target(bann_ctx* ctx, int32_t b, const float* y) {
+  if (!check_branch(ctx, b) || !y) return fail(ctx, BANN_E_ARG, "bad branch or null target");
+  CK(hipMemcpyAsync(ctx->d_y + (int64_t)b * ctx->n, y, ctx->n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_set_target_all(bann_ctx* ctx, const float* y) {
+  if (!ctx || !ctx->finalized || !y) return fail(ctx, BANN_E_ARG, "not finalized or null target");
+  for (size_t b = 0; b < ctx->br.size(); ++b)
+    CK(hipMemcpyAsync(ctx->d_y + (int64_t)b * ctx->n, y, ctx->n * sizeof(float), hipMemcpyHostToDevice,
+                      ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// per-branch math
+// ---------------------------------------------------------------------------
+static int eval_branch(bann_ctx* ctx, int32_t b, int write_pred) {
+  Plan p;
+  int rc = build_plan(ctx, &b, 1, p, false);
+  if (rc) return rc;
+  rc = run_grad(ctx, p, write_pred);
+  if (rc) return rc;
+  launch_update(ctx->st, p.d_all, 1, MODE_GRAD, 0, ctx->stream);
+  CK(hipGetLastError());
+  return BANN_OK;
+}
+
+extern "C" int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out) {
+  if (!check_branch(ctx, b) || !pred_out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  int rc = eval_branch(ctx, b, 1);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(pred_out, ctx->d_pred + (int64_t)b * ctx->n, ctx->n * sizeof(float), hipMemcpyDeviceToHost,
+                    ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_rss(bann_ctx* ctx, int32_t b, double* rss_out) {
+  if (!check_branch(ctx, b) || !rss_out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  int rc = eval_branch(ctx, b, 0);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(rss_out, ctx->d_rss + b, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_log_density_gradient(bann_ctx* ctx, int32_t b, float* grad_out, double* rss_out) {
+  if (!check_branch(ctx, b) || !grad_out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  int rc = eval_branch(ctx, b, 0);
+  if (rc) return rc;
+  const BranchHost& h = ctx->br[b];
+  CK(hipMemcpyAsync(grad_out, ctx->d_grad + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  if (rss_out) CK(hipMemcpyAsync(rss_out, ctx->d_rss + b, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+// host evaluation of log_density at the current parameters (branch_sampler.rs:72-78)
+static int host_log_density(bann_ctx* ctx, int32_t b, double rss, double* out) {
+  const BranchHost& h = ctx->br[b];
+  std::vector<float> th(h.P), lam, lamld;
+  CK(hipMemcpyAsync(th.data(), ctx->d_theta + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  float ep = 1.f;
+  expand_precisions(h, lam, lamld, ep);
+  const bool lasso = (h.prior == BANN_LASSO_ARD || h.prior == BANN_LASSO_BASE);
+  double ld = 0.0;
+  for (int i = 0; i < h.P; ++i)
+    ld -= lasso ? (double)lamld[i] * fabs((double)th[i]) : 0.5 * (double)lamld[i] * (double)th[i] * (double)th[i];
+  *out = ld - (double)ep * rss / 2.0;
+  return BANN_OK;
+}
+
+extern "C" int bann_log_density(bann_ctx* ctx, int32_t b, double rss, double* out) {
+  if (!check_branch(ctx, b) || !out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  return host_log_density(ctx, b, rss, out);
+}
+
+extern "C" int bann_neg_hamiltonian(bann_ctx* ctx, int32_t b, const float* momentum, double* out) {
+  if (!check_branch(ctx, b) || !momentum || !out) return fail(ctx, BANN_E_ARG, "bad branch or null pointer");
+  double rss = 0.0;
+  int rc = bann_rss(ctx, b, &rss);
+  if (rc) return rc;
+  double ld = 0.0;
+  rc = host_log_density(ctx, b, rss, &ld);
+  if (rc) return rc;
+  double k = 0.0;
+  for (int64_t i = 0; i < ctx->br[b].P; ++i) k += (double)momentum[i] * (double)momentum[i];
+  *out = ld - 0.5 * k;
+  return BANN_OK;
+}
+
+// ---------------------------------------------------------------------------
+// HMC
+// ---------------------------------------------------------------------------
+static int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
+                        const float* eps, const float* momentum, uint64_t seed, const float* u) {
+  int rc = ensure_htrace(ctx, L);
+  if (rc) return rc;
+  ctx->st.max_dh = max_dh;
+  ctx->st.lint = ctx->htrace_cap - 1;
+  std::mt19937_64 rng(seed ^ 0x5DEECE66Dull);
+  std::vector<float> e;
+  int64_t off = 0;
+  for (int32_t b : p.all) {
+    const BranchHost& h = ctx->br[b];
+    if (step_mode == BANN_STEP_INJECTED) {
+      if (!eps) return fail(ctx, BANN_E_ARG, "injected step sizes need eps");
+      CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, eps + off, h.P * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+    } else {
+      if (step_mode != BANN_STEP_UNIFORM && step_mode != BANN_STEP_RANDOM && step_mode != BANN_STEP_IZMAILOV)
+        return fail(ctx, BANN_E_ARG, "unsupported step size mode (StdScaled is not usable in the reference either)");
+      host_step_sizes(h, step_mode, factor, L, rng, e);
+      CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, e.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+    }
+    if (momentum)
+      CK(hipMemcpyAsync(ctx->d_mom + h.dev.p_off, momentum + off, h.P * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+    off += h.P;
+  }
+  if (!momentum) {
+    launch_sample_momentum(ctx->st, p.d_all, (int32_t)p.all.size(), p.max_p, seed, ctx->stream);
+    CK(hipGetLastError());
+  }
+  std::vector<float> uu(ctx->br.size(), 0.f);
+  std::uniform_real_distribution<float> U(0.f, 1.f);
+  for (size_t i = 0; i < p.all.size(); ++i) uu[p.all[i]] = u ? u[i] : U(rng);
+  CK(hipMemcpyAsync(ctx->d_u, uu.data(), uu.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+  return BANN_OK;
+}
+
+extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
+                             int32_t step_mode, float factor, const float* eps, const float* momentum, uint64_t seed,
+                             const float* u, int32_t* status_out, double* h_trace_out, int32_t* uturn_out,
+                             double* log_density_out) {
+  if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (!branches || nb <= 0 || L < 0) return fail(ctx, BANN_E_ARG, "bad branch list or L");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  for (int i = 0; i < nb; ++i)
+    for (int k = 0; k < i; ++k)
+      if (branches[i] == branches[k]) return fail(ctx, BANN_E_ARG, "duplicate branch in list");
+  Plan p;
+  int rc = build_plan(ctx, branches, nb, p, false);
+  if (rc) return rc;
+  rc = traj_prepare(ctx, p, std::max(L, 1), max_dh, step_mode, factor, eps, momentum, seed, u);
+  if (rc) return rc;
+  rc = run_grad(ctx, p, L == 0 ? 1 : 0);
+  if (rc) return rc;
+  if (L == 0) {  // empty leapfrog loop: accept_or_reject at the initial state accepts
+    launch_update(ctx->st, p.d_all, nb, MODE_GRAD, 0, ctx->stream);
+    CK(hipGetLastError());
+    CK(hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < nb; ++i) {
+      if (status_out) status_out[i] = BANN_ACCEPTED;
+      if (uturn_out) uturn_out[i] = -1;
+    }
+    if (log_density_out)
+      for (int i = 0; i < nb; ++i)
+        CK(hipMemcpy(log_density_out + i, ctx->d_ld + branches[i], sizeof(double), hipMemcpyDeviceToHost));
+    return BANN_OK;
+  }
+  launch_update(ctx->st, p.d_all, nb, MODE_INIT, 0, ctx->stream);
+  for (int k = 1; k <= L; ++k) {
+    rc = run_grad(ctx, p, k == L ? 1 : 0);
+    if (rc) return rc;
+    launch_update(ctx->st, p.d_all, nb, k < L ? MODE_STEP : MODE_LAST, k, ctx->stream);
+  }
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  const int stride = ctx->htrace_cap;
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
+    if (status_out) CK(hipMemcpy(status_out + i, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (uturn_out) CK(hipMemcpy(uturn_out + i, ctx->d_uturn + b, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (log_density_out) CK(hipMemcpy(log_density_out + i, ctx->d_ld + b, sizeof(double), hipMemcpyDeviceToHost));
+    if (h_trace_out)
+      CK(hipMemcpy(h_trace_out + (int64_t)i * (L + 1), ctx->d_htrace + (int64_t)b * stride, (L + 1) * sizeof(double),
+                   hipMemcpyDeviceToHost));
+  }
+  return BANN_OK;
+}
+
+extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
+                                   int32_t step_mode, float factor, uint64_t seed) {
+  if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (!branches || nb <= 0 || L < 1) return fail(ctx, BANN_E_ARG, "bad branch list or L");
+  int rc = build_plan(ctx, branches, nb, ctx->lf, true);
+  if (rc) return rc;
+  rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
+  if (rc) return rc;
+  rc = run_grad(ctx, ctx->lf, 0);
+  if (rc) return rc;
+  launch_update(ctx->st, ctx->lf.d_all, nb, MODE_INIT, 0, ctx->stream);
+  CK(hipGetLastError());
+  ctx->lf_active = true;
+  ctx->lf_L = L;
+  ctx->lf_step = 0;
+  return BANN_OK;
+}
+
+extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
+  if (!ctx || !ctx->lf_active) return fail(ctx, BANN_E_STATE, "no leapfrog session");
+  if (k < 0 || ctx->lf_step + k > ctx->lf_L) return fail(ctx, BANN_E_ARG, "steps beyond the trajectory length");
+  const int32_t nb = (int32_t)ctx->lf.all.size();
+  for (int i = 0; i < k; ++i) {
+    const int step = ++ctx->lf_step;
+    int rc = run_grad(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0);
+    if (rc) return rc;
+    launch_update(ctx->st, ctx->lf.d_all, nb, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step, ctx->stream);
+  }
+  CK(hipGetLastError());
+  return BANN_OK;
+}
+
+extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* num_accepted) {
+  if (!ctx || !ctx->lf_active) return fail(ctx, BANN_E_STATE, "no leapfrog session");
+  if (ctx->lf_step != ctx->lf_L) {
+    int rc = bann_leapfrog_steps(ctx, ctx->lf_L - ctx->lf_step);
+    if (rc) return rc;
+  }
+  CK(hipStreamSynchronize(ctx->stream));
+  std::vector<int32_t> st(ctx->br.size());
+  CK(hipMemcpy(st.data(), ctx->d_status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int acc = 0;
+  for (size_t i = 0; i < ctx->lf.all.size(); ++i) {
+    const int s = st[ctx->lf.all[i]];
+    if (status_out) status_out[i] = s;
+    acc += s == BANN_ACCEPTED;
+  }
+  if (num_accepted) *num_accepted = acc;
+  ctx->lf_active = false;
+  return BANN_OK;
+}
+
+extern "C" int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out) {
+  if (!ctx || !out) return BANN_E_ARG;
+  *out = ctx->d_pred;
+  return BANN_OK;
+}

@@ -1,0 +1,112 @@
+// bann_internal.h — device-visible descriptors and launcher declarations shared
+// by the HIP kernels (kernels_*.hip) and the C-ABI implementation (bann_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define BANN_MAXL 8          // max layers per branch (hidden + summary + output)
+#define BANN_FUSED_MAXW 4    // fused kernel: every layer width <= 4
+#define BANN_FUSED_MAXCH 16  // fused kernel: <= 16 marker chunks of 64 (m_b <= 1024)
+#define BANN_CHUNK 64        // markers per chunk (one 16x16x64 i8 MFMA K-step)
+#define BANN_FRAG 16         // individuals per fragment (MFMA N)
+#define BANN_TILE_FRAGS 4    // fragments per fused-kernel tile (64 individuals)
+
+enum { MODE_GRAD = 0, MODE_INIT = 1, MODE_STEP = 2, MODE_LAST = 3 };
+enum { ST_RUNNING = -1, ST_ACCEPTED = 0, ST_REJECTED = 1, ST_REJECTED_EARLY = 2 };
+
+// Per-branch descriptor (device resident, one per branch).
+struct BranchDev {
+  int64_t x_off;      // byte offset of the packed genotype block
+  int64_t p_off;      // offset into the params-sized arrays (theta, p, eps, ...)
+  int64_t mk_off;     // offset into per-branch marker arrays (mu/sigma gathered), m entries
+  int64_t part_off;   // float offset into the partial-gradient slabs: nsplits x P
+  int64_t dig_off;    // byte offset of the MFMA A-operand digits [nchunks][64][16]
+  int64_t y_off;      // offset of the target / prediction vectors (b * n)
+  int64_t scr_off;    // float offset into the generic-path scratch
+  int32_t m;          // markers in the branch
+  int32_t nchunks;    // ceil(m / 64)
+  int32_t L;          // number of layers (weight matrices)
+  int32_t act;        // bann_activation
+  int32_t prior;      // bann_prior
+  int32_t P;          // num params
+  int32_t nsplits;    // row splits (partial slabs)
+  int32_t fused;      // 1 = fused kernel path
+  int32_t widths[BANN_MAXL];  // out width of each layer (last = 1)
+  int32_t win[BANN_MAXL];     // in width of each layer (win[0] = m)
+  int32_t woff[BANN_MAXL];    // param_vec offset of W_l
+  int32_t boff[BANN_MAXL];    // param_vec offset of b_l (l < L-1)
+  int32_t scr_z[BANN_MAXL];   // generic scratch: per-layer offsets (x n) of z_l
+  int32_t scr_a[BANN_MAXL];   //   a_l
+  int32_t scr_d[BANN_MAXL];   //   delta_l
+  int32_t scr_stride;         //   floats per individual
+};
+
+// One work item of the fused gradient kernel: a contiguous fragment range of one branch.
+struct GradItem {
+  int32_t branch;
+  int32_t split;
+  int32_t frag_begin;
+  int32_t frag_end;
+};
+
+// Per-branch derived constants of the fused path (rewritten after every position update).
+struct FusedConst {
+  float scale[BANN_FUSED_MAXW];  // power-of-two scale of the W0/sigma digits per column
+  float c0[BANN_FUSED_MAXW];     // b0_k - sum_j mu_j W0_jk / sigma_j
+};
+
+struct DevState {
+  const BranchDev* br;    // [nbranch]
+  const int8_t* xpk;      // packed genotypes
+  const uint8_t* dig;     // digits
+  FusedConst* fc;         // [nbranch]
+  const float* mu;        // gathered per-branch marker means  [sum m]
+  const float* sigma;     // gathered per-branch marker stds
+  float* theta;           // [sum P]
+  float* mom;             // momentum
+  float* eps;             // step sizes
+  float* theta0;          // trajectory start
+  float* lam;             // per-parameter gradient precision multiplier
+  float* lamld;           // per-parameter log-density multiplier
+  float* grad;            // scratch: log density gradient
+  float* part;            // partial d(rss/2) slabs
+  double* rss_part;       // [nbranch][max splits]
+  float* y;               // targets [nbranch][n]
+  float* pred;            // predictions [nbranch][n]
+  float* scr;             // generic-path scratch
+  float* eprec;           // error precision per branch
+  double* h0;             // initial -H per branch
+  double* htrace;         // [nbranch][Lint+1]
+  double* ld_out;         // log density per branch (last evaluation)
+  double* rss_out;        // rss per branch (last evaluation)
+  int32_t* status;        // per-branch trajectory status
+  int32_t* uturn;         // first U-turn step
+  float* uacc;            // acceptance uniforms per branch
+  int64_t n;              // individuals
+  int32_t nfrag;          // ceil(n / 16)
+  int32_t max_splits;
+  int32_t lint;           // trajectory length L (for the trace stride)
+  float max_dh;
+};
+
+// ---- launchers (defined in the kernel translation units) ----
+void launch_synthetic_genotypes(int8_t* g, float* mu, float* sigma, int64_t n, int64_t M, uint64_t seed,
+                                hipStream_t s);
+void launch_decode_bed(const uint8_t* payload, int8_t* g, int64_t n, int64_t M, hipStream_t s);
+void launch_col_stats(const int8_t* g, float* mu, float* sigma, int64_t n, int64_t M, hipStream_t s);
+void launch_pack_branch(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* dst, int32_t nchunks,
+                        int32_t nfrag, hipStream_t s);
+void launch_unpack_markers(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* out,
+                           hipStream_t s);
+void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp_idx, int32_t m, float* mu_b,
+                         float* sig_b, hipStream_t s);
+
+void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
+                       int write_pred, hipStream_t s);
+void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
+                         hipStream_t s);
+void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
+                   hipStream_t s);
+void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
+void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
+                            hipStream_t s);

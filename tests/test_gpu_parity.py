@@ -1,0 +1,323 @@
+"""GPU parity of the HIP hot path against the CPU oracle (and the reference KATs).
+
+Every test calls through the C ABI (librsbann_amd.so via ctypes).  The oracle
+(oracle/bann_oracle.py, float64) gets the SAME genotypes (downloaded from the
+device), the same standardization constants and the f32-rounded parameters.
+
+Tolerances (north_star: gradients and log-posterior within 1e-5 relative):
+  * gradient tensors (per layer, weights and biases), predictions: norm-relative
+    ||gpu - oracle|| / ||oracle|| <= 1e-5, on unsaturated synthetic inputs
+    (standardized X, W ~ N(0, 1/m)).
+  * rss, log density, -H: |gpu - oracle| <= 1e-5 * max(1, |oracle|).
+  * reference KATs (saturated tanh): the per-tensor tolerances derived in
+    tests/test_oracle_kats.py (1e-5, or the f32 cancellation bound ~1e-3 for the
+    bias gradients).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import bann_oracle as O
+from helpers import build_context, f32_branch, layer_views, norm_rel, x_std
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KAT = json.load(open(os.path.join(HERE, "golden", "reference_kats.json")))
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def Ctx():
+    from bann import BannContext
+    return BannContext
+
+
+def scalar_close(a, b, tol=TOL):
+    return abs(a - b) <= tol * max(1.0, abs(b))
+
+
+# ---------------------------------------------------------------- KATs on GPU
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("prior", ["ridge_ard", "ridge_base", "lasso_ard", "lasso_base"])
+def test_kat_gradient_gpu(Ctx, prior, fused):
+    from test_oracle_kats import cancellation_tol
+    X, y = O.kat_data()
+    exp = KAT[prior]["ldg"]
+    br = O.kat_branch(prior, exp["precision"])
+    g = X.T.astype(np.int8)  # raw genotypes; mu = 0, sigma = 1 -> X_std == X
+    ctx = build_context(Ctx, g, [dict(snps=[0, 1, 2], branch=br, y=y)], fused=fused,
+                        stats=(np.zeros(3), np.ones(3)))
+    assert ctx.kernel_path(0) == ("fused" if fused else "generic")
+    grad, rss = ctx.log_density_gradient(0)
+    gw, gb = layer_views(br, grad)
+    for l in range(3):
+        assert norm_rel(gw[l].reshape(-1, order="F"), exp["wrt_w"][l]) < TOL, (l, gw[l])
+    for l in range(2):
+        assert norm_rel(gb[l], exp["wrt_b"][l]) < cancellation_tol(br, X, l), (l, gb[l])
+    assert scalar_close(rss, KAT["rss"])
+    pred = ctx.predict(0)
+    assert norm_rel(pred, KAT["forward_feed"]["out"]) < 1e-6
+    ctx.close()
+
+
+# ------------------------------------------------------ random-config parity
+CONFIGS = [
+    dict(n=1000, m=100, widths=[4, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=333, m=77, widths=[3, 2, 1], act="relu", prior="lasso_ard"),
+    dict(n=500, m=130, widths=[4, 1], act="silu", prior="ridge_base"),
+    dict(n=257, m=64, widths=[4, 4, 4, 1], act="leaky_relu", prior="lasso_base"),
+    dict(n=100, m=5, widths=[2, 2, 1], act="identity", prior="std_normal"),
+    dict(n=2000, m=500, widths=[4, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=700, m=1000, widths=[4, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=300, m=1100, widths=[4, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=400, m=60, widths=[8, 8, 1], act="tanh", prior="ridge_ard"),
+    dict(n=1000, m=100, widths=[50, 50, 1], act="tanh", prior="ridge_ard"),
+    dict(n=1, m=3, widths=[2, 1], act="tanh", prior="ridge_base"),
+]
+
+
+def make_problem(cfg, seed):
+    rng = np.random.default_rng(seed)
+    n, m = cfg["n"], cfg["m"]
+    M = m + 7
+    g = O.synthetic_genotypes(rng, n, M)
+    snps = rng.permutation(M)[:m].astype(np.int32)
+    br = f32_branch(O.random_branch(rng, m, cfg["widths"], prior=cfg["prior"], act=cfg["act"]))
+    return rng, g, snps, br
+
+
+def oracle_inputs(ctx, g, snps):
+    mu, sd = ctx.genotype_stats()
+    X = x_std(g[snps], mu[snps], sd[snps])
+    return X
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("ci", range(len(CONFIGS)))
+def test_gradient_parity(Ctx, ci, fused):
+    cfg = CONFIGS[ci]
+    rng, g, snps, br = make_problem(cfg, 100 + ci)
+    # y near the branch's own prediction (h^2 ~ 0.5 style residual)
+    ctx0 = None
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(cfg["n"]))], fused=fused)
+    X = oracle_inputs(ctx, g, snps)
+    f = O.predict(br, X)
+    y = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=cfg["n"])).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    if fused and cfg["widths"][0] <= 4 and max(cfg["widths"]) <= 4 and cfg["m"] <= 1024 and len(cfg["widths"]) <= 4:
+        assert ctx.kernel_path(0) == "fused"
+    else:
+        assert ctx.kernel_path(0) == "generic"
+    grad, rss = ctx.log_density_gradient(0)
+    ogw, ogb, orss = O.log_density_gradient(br, X, y)
+    gw, gb = layer_views(br, grad)
+    for l in range(br.num_layers):
+        assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
+    for l in range(br.num_layers - 1):
+        assert norm_rel(gb[l], ogb[l]) < TOL, ("b", l, norm_rel(gb[l], ogb[l]))
+    assert scalar_close(rss, orss), (rss, orss)
+    pred = ctx.predict(0)
+    assert norm_rel(pred, f) < TOL
+    ld = ctx.log_density(0, rss)
+    assert scalar_close(ld, O.log_density(br, orss))
+    p = rng.normal(size=br.num_params)
+    assert scalar_close(ctx.neg_hamiltonian(0, p.astype(np.float32)),
+                        O.log_density(br, orss) - 0.5 * float(np.sum(p.astype(np.float32).astype(np.float64) ** 2)))
+    ctx.close()
+
+
+def test_multi_branch_packed(Ctx):
+    """Several branches of mixed shape/prior/path in one context (overlapping
+    marker groups, as external.rs allows): every branch's gradient matches."""
+    rng = np.random.default_rng(7)
+    n, M = 777, 1500
+    g = O.synthetic_genotypes(rng, n, M)
+    shapes = [(500, [4, 4, 1], "tanh", "ridge_ard"), (64, [4, 1], "relu", "lasso_base"),
+              (300, [2, 2, 1], "silu", "ridge_base"), (40, [6, 3, 1], "tanh", "lasso_ard"),
+              (1024, [4, 4, 1], "tanh", "ridge_ard"), (200, [4, 4, 4, 1], "leaky_relu", "std_normal")]
+    specs = []
+    for m, w, a, p in shapes:
+        snps = rng.choice(M, size=m, replace=False).astype(np.int32)
+        br = f32_branch(O.random_branch(rng, m, w, prior=p, act=a))
+        specs.append(dict(snps=snps, branch=br, y=rng.normal(size=n).astype(np.float32).astype(np.float64)))
+    ctx = build_context(Ctx, g, specs)
+    mu, sd = ctx.genotype_stats()
+    for b, s in enumerate(specs):
+        X = x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]])
+        grad, rss = ctx.log_density_gradient(b)
+        ogw, ogb, orss = O.log_density_gradient(s["branch"], X, s["y"])
+        assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL, b
+        assert scalar_close(rss, orss)
+    ctx.close()
+
+
+def test_gradient_deterministic_and_split_invariant(Ctx):
+    rng, g, snps, br = make_problem(dict(n=4000, m=500, widths=[4, 4, 1], act="tanh", prior="ridge_ard"), 3)
+    y = rng.normal(size=4000)
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=y)])
+    g1, r1 = ctx.log_density_gradient(0)
+    g2, r2 = ctx.log_density_gradient(0)
+    assert np.array_equal(g1, g2) and r1 == r2  # fixed-order reductions: bitwise reproducible
+    ctx.close()
+    os.environ["BANN_TARGET_ITEMS"] = "1"      # one split instead of many
+    try:
+        ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=y)])
+        g3, r3 = ctx.log_density_gradient(0)
+    finally:
+        del os.environ["BANN_TARGET_ITEMS"]
+    assert norm_rel(g3, g1) < 1e-6 and abs(r3 - r1) < 1e-6 * abs(r1)
+    ctx.close()
+
+
+# ----------------------------------------------------------------- HMC parity
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("prior", ["ridge_ard", "lasso_base", "std_normal"])
+def test_hmc_step_parity(Ctx, prior, fused):
+    """hmc_step (branch_sampler.rs:1192-1299) with injected momentum, step sizes
+    and acceptance uniform: same trajectory, -H trace, status and end state."""
+    rng = np.random.default_rng(11)
+    n, m, L = 600, 120, 6
+    g = O.synthetic_genotypes(rng, n, m)
+    snps = np.arange(m, dtype=np.int32)
+    br = f32_branch(O.random_branch(rng, m, [4, 4, 1], prior=prior, act="tanh"))
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(n))], fused=fused)
+    X = oracle_inputs(ctx, g, snps)
+    y = (O.predict(br, X) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    ew, eb = O.izmailov_step_sizes(br, 0.5, L)
+    eps = O.param_vec(ew, eb).astype(np.float32)
+    p0 = rng.normal(size=br.num_params).astype(np.float32)
+    res = ctx.hmc_step([0], L, 10.0, eps=eps, momentum=p0, u=[0.5])
+    ow, ob = O.load_param_vec(eps.astype(np.float64), m, br.layer_widths)
+    pw, pb = O.load_param_vec(p0.astype(np.float64), m, br.layer_widths)
+    ob_ = br.copy()
+    out = O.hmc_step(ob_, X, y, ow, ob, pw, pb, L, 10.0, 0.5)
+    assert res["status"][0] == out["status"]
+    tr = np.asarray(out["trace"])
+    gt = res["trace"][0][: tr.size]
+    assert np.all(np.abs(gt - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (gt, tr)
+    final = ctx.get_params(0)
+    assert norm_rel(final, O.param_vec(ob_.weights, ob_.biases)) < 1e-5
+    assert res["uturn"][0] == out["u_turn_step"]
+    ctx.close()
+
+
+def test_hmc_early_rejection_restores(Ctx):
+    """|dH| > max_hamiltonian_error -> RejectedEarly and initial params restored (1264-1279)."""
+    rng = np.random.default_rng(5)
+    n, m = 300, 64
+    g = O.synthetic_genotypes(rng, n, m)
+    br = f32_branch(O.random_branch(rng, m, [4, 4, 1]))
+    ctx = build_context(Ctx, g, [dict(snps=np.arange(m), branch=br, y=rng.normal(size=n))])
+    before = ctx.get_params(0)
+    eps = np.full(br.num_params, 5.0, np.float32)   # absurd step sizes
+    res = ctx.hmc_step([0], 4, 0.1, eps=eps, momentum=np.ones(br.num_params, np.float32), u=[0.0])
+    assert res["status"][0] == 2
+    assert np.array_equal(ctx.get_params(0), before)
+    ctx.close()
+
+
+def test_hmc_packed_equals_individual(Ctx):
+    """Packing branches into one launch does not change any branch's trajectory."""
+    rng = np.random.default_rng(9)
+    n, M = 400, 300
+    g = O.synthetic_genotypes(rng, n, M)
+    specs = []
+    for k in range(4):
+        snps = rng.choice(M, size=100, replace=False).astype(np.int32)
+        br = f32_branch(O.random_branch(rng, 100, [4, 4, 1]))
+        specs.append(dict(snps=snps, branch=br, y=rng.normal(size=n)))
+    P = specs[0]["branch"].num_params
+    eps = np.concatenate([O.param_vec(*O.izmailov_step_sizes(s["branch"], 0.3, 5)) for s in specs]).astype(np.float32)
+    p0 = rng.normal(size=4 * P).astype(np.float32)
+    u = np.array([0.3, 0.6, 0.9, 0.1], np.float32)
+    ctx = build_context(Ctx, g, specs)
+    r_all = ctx.hmc_step([0, 1, 2, 3], 5, 10.0, eps=eps, momentum=p0, u=u)
+    params_all = [ctx.get_params(b) for b in range(4)]
+    ctx.close()
+    for b in range(4):
+        ctx = build_context(Ctx, g, specs)
+        r1 = ctx.hmc_step([b], 5, 10.0, eps=eps[b * P:(b + 1) * P], momentum=p0[b * P:(b + 1) * P], u=u[b:b + 1])
+        assert r1["status"][0] == r_all["status"][b]
+        assert np.array_equal(ctx.get_params(b), params_all[b])
+        assert np.array_equal(r1["trace"][0], r_all["trace"][b])
+        ctx.close()
+
+
+def test_leapfrog_session_matches_hmc_step(Ctx):
+    """The benchmark entry points (begin/steps/end, device RNG) run the same
+    integrator: with L steps they leave every branch accepted/rejected with
+    finite traces and params either moved or restored."""
+    rng = np.random.default_rng(21)
+    n, M, nb = 512, 640, 5
+    g = O.synthetic_genotypes(rng, n, M)
+    specs = []
+    for b in range(nb):
+        snps = np.arange(b * 128, (b + 1) * 128, dtype=np.int32)
+        br = f32_branch(O.random_branch(rng, 128, [4, 4, 1]))
+        specs.append(dict(snps=snps, branch=br, y=rng.normal(size=n)))
+    ctx = build_context(Ctx, g, specs)
+    before = [ctx.get_params(b) for b in range(nb)]
+    ctx.leapfrog_begin(list(range(nb)), 8, 10.0, "izmailov", 0.5, seed=3)
+    ctx.leapfrog_steps(3)
+    ctx.leapfrog_steps(5)
+    status, acc = ctx.leapfrog_end()
+    assert acc == int(np.sum(status == 0))
+    for b in range(nb):
+        after = ctx.get_params(b)
+        assert np.all(np.isfinite(after))
+        if status[b] != 0:
+            assert np.array_equal(after, before[b])
+    ctx.close()
+
+
+# ------------------------------------------------------------ genotype ingestion
+def test_bed_decode_gpu(Ctx):
+    bs = KAT["bed_small"]
+    ctx = Ctx(0)
+    ctx.upload_bed(bytes.fromhex(bs["bed_payload_hex"]), bs["n"], bs["m"])
+    g = ctx.download_genotypes(np.arange(bs["m"]))
+    assert np.array_equal(g.reshape(-1).astype(np.float32), np.array(bs["data_f32_col_major"], np.float32))
+    mu, sd = ctx.genotype_stats()
+    assert np.allclose(mu, bs["col_means"], rtol=0, atol=1e-6)
+    assert np.allclose(sd, bs["col_stds"], rtol=1e-6, atol=1e-7)
+    ctx.close()
+
+
+def test_synthetic_genotypes_gpu(Ctx):
+    ctx = Ctx(0)
+    n, M = 5000, 300
+    ctx.synthetic_genotypes(n, M, seed=42)
+    g = ctx.download_genotypes(np.arange(M))
+    assert set(np.unique(g)) <= {0, 1, 2}
+    mu, sd = ctx.genotype_stats()
+    assert np.all(sd > 0)                                   # zero-variance markers redrawn
+    assert np.allclose(mu, g.mean(axis=1), atol=1e-6)
+    assert np.allclose(sd, g.astype(np.float64).std(axis=1), rtol=1e-5)
+    p = mu / 2
+    assert p.min() > 0.0 and p.max() < 0.56                 # p_j ~ U(0.01, 0.5)
+    ctx2 = Ctx(0)
+    ctx2.synthetic_genotypes(n, M, seed=42)
+    assert np.array_equal(ctx2.download_genotypes(np.arange(M)), g)   # counter-based: reproducible
+    ctx.close()
+    ctx2.close()
+
+
+def test_error_paths(Ctx):
+    from bann import BannError
+    ctx = Ctx(0)
+    with pytest.raises(BannError):
+        ctx.finalize()                                      # no genotypes
+    ctx.synthetic_genotypes(64, 10)
+    with pytest.raises(BannError):
+        ctx.add_branch([0, 11], [4, 1])                     # marker out of range
+    with pytest.raises(BannError):
+        ctx.add_branch([0, 1], [4, 2])                      # output width != 1
+    ctx.add_branch([0, 1, 2], [2, 1])
+    ctx.finalize()
+    with pytest.raises(BannError):
+        ctx.add_branch([0], [1, 1])                         # after finalize
+    ctx.close()
