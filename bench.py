@@ -1,0 +1,252 @@
+#!/usr/bin/env python3
+"""HMC leapfrog steps/sec on the BASELINE.json cohort (C3: 50k individuals x
+500k SNPs x 1k branches of 500 SNPs; D = 1, W = S = 4; RidgeARD, tanh).
+
+One "step" = one full-cohort leapfrog step: a packed gradient evaluation of
+every branch (one fused HIP launch) + the fused momentum/position/-H update
+(one launch).  Genotypes are synthetic (generated on the device), resident in
+HBM as int8 before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  (N > 1: launched by torch.distributed.run, one rank per GPU; the 1k branches
+   are sharded over the ranks, no collective inside a step; the trajectory end
+   all-reduces the n-vector residual change over RCCL.)
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rs-bann_amd"))
+
+CONFIGS = {
+    # name: (n, total SNPs, branches, layer_widths)
+    "c3": (50_000, 500_000, 1000, [4, 4, 1]),
+    "c2": (10_000, 128_000, 64, [4, 4, 1]),
+    "small": (8_192, 64_000, 128, [4, 4, 1]),
+}
+METRIC = "HMC leapfrog steps/sec (whole node), 50k indiv × 500k SNP × 1k branches"
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def init_branch_params(rng, m, widths):
+    """default init (branch_cfg_builder.rs:180-186): W ~ N(0, 1/m); biases small
+    random; ARD ML precisions (308-328); bias ML precisions (264-274)."""
+    ins = [m] + widths[:-1]
+    ws = [rng.normal(0.0, math.sqrt(1.0 / m), size=(i, o)) for i, o in zip(ins, widths)]
+    bs = [rng.normal(0.0, 0.1, size=o) for o in widths[:-1]]
+    pv = np.concatenate([w.reshape(-1, order="F") for w in ws] + bs).astype(np.float32)
+    prec = []
+    for l, w in enumerate(ws[:-1]):
+        prec.append(widths[l] / np.sum(w * w, axis=1))
+    prec.append(np.array([0.0]))  # output precision: set globally below (architectures.rs:175-185)
+    prec += [np.array([b.size / np.sum(b * b)]) for b in bs]
+    prec.append(np.array([2.0]))  # error precision (branch_cfg_builder.rs:394)
+    return pv, prec, float(np.sum(ws[-1] ** 2))
+
+
+def cpu_baseline(n, m, widths, sample_branches, sample_steps):
+    lib_path = os.path.join(ROOT, "oracle", "libbann_ref_cpu.so")
+    if not os.path.exists(lib_path):
+        return None
+    L = ctypes.CDLL(lib_path)
+    f = L.bann_ref_cpu_bench
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    setup, cs = ctypes.c_double(), ctypes.c_double()
+    t = f(n, m, widths[0], widths[1], sample_branches, sample_steps, 42, threads, ctypes.byref(setup),
+          ctypes.byref(cs))
+    if t <= 0:
+        return None
+    branch_steps_per_s = sample_branches * sample_steps / t
+    return dict(branch_steps_per_s=branch_steps_per_s, threads=threads, seconds=t, setup_s=setup.value)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--step-factor", type=float, default=0.5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-branches", type=int, default=16)
+    ap.add_argument("--cpu-sample-steps", type=int, default=3)
+    ap.add_argument("--profile-iters", type=int, default=10)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local_rank)
+        dist_mod.init_process_group("nccl", init_method="env://")
+        dist = dist_mod
+
+    from bann import BannContext
+
+    n, M_total, B_total, widths = CONFIGS[args.config]
+    m_b = M_total // B_total
+    b0, b1 = rank * B_total // world, (rank + 1) * B_total // world
+    nb = b1 - b0
+    L = args.warmup + args.steps
+
+    t_setup = time.time()
+    ctx = BannContext(local_rank)
+    # this rank's markers only (uniform contiguous grouping, uniform.rs:11-23)
+    ctx.synthetic_genotypes(n, nb * m_b, seed=1000003 * (rank + 1))
+    for k in range(nb):
+        ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
+    ctx.finalize(free_raw=True)
+    assert all(ctx.kernel_path(k) == "fused" for k in range(nb))
+    params, precs, out_ss = [], [], 0.0
+    for k in range(nb):
+        rng = np.random.default_rng(b0 + k)
+        pv, prec, ss = init_branch_params(rng, m_b, widths)
+        params.append(pv)
+        precs.append(prec)
+        out_ss += ss
+    tot = np.array([out_ss, float(nb)])
+    if dist is not None:
+        import torch
+        tt = torch.tensor(tot, device="cuda")
+        dist.all_reduce(tt)
+        tot = tt.cpu().numpy()
+    out_prec = tot[1] / tot[0]
+    fsum = np.zeros(n, np.float64)
+    for k in range(nb):
+        prec = precs[k]
+        prec[len(widths) - 1] = np.array([out_prec])
+        ctx.set_params(k, params[k])
+        ctx.set_precisions(k, np.concatenate(prec).astype(np.float32))
+    preds = []
+    for k in range(nb):
+        p = ctx.predict(k)
+        preds.append(p)
+        fsum += p
+    if dist is not None:
+        import torch
+        tt = torch.tensor(fsum, device="cuda")
+        dist.all_reduce(tt)
+        fsum = tt.cpu().numpy()
+    # phenotype y = sum_b f_b + noise at h^2 = 0.5; residual = noise; each branch
+    # is fitted to its partial residual residual + f_b (net.rs:279-280)
+    noise = np.random.default_rng(7).normal(0.0, max(float(np.std(fsum)), 1e-3), size=n)
+    for k in range(nb):
+        ctx.set_target(k, (noise + preds[k]).astype(np.float32))
+    del preds
+    ctx.synchronize()
+    setup_s = time.time() - t_setup
+
+    import torch
+    delta = None
+    if torch.cuda.is_available():   # initialise torch/HIP state before the timed region
+        delta = torch.zeros(n, dtype=torch.float32, device=f"cuda:{local_rank}")
+        torch.cuda.synchronize()
+    branches = list(range(nb))
+    ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=11 + rank)
+    if args.warmup:
+        ctx.leapfrog_steps(args.warmup)
+    ctx.synchronize()
+    if dist is not None:
+        import torch
+        torch.cuda.synchronize()
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctx.leapfrog_steps(args.steps)
+    status, acc = ctx.leapfrog_end()          # final half step + Metropolis (device)
+    # residual update of the sweep: all-reduce of the n-vector over ranks (RCCL)
+    if delta is not None:
+        ctx.residual_delta_device(delta.data_ptr())
+        if dist is not None:
+            dist.all_reduce(delta)
+        torch.cuda.synchronize()
+    ctx.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        te = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+        ta = torch.tensor([acc, nb], device="cuda", dtype=torch.float64)
+        dist.all_reduce(ta)
+        acc_all, nb_all = float(ta[0]), float(ta[1])
+    else:
+        acc_all, nb_all = float(acc), float(nb)
+
+    # ---- kernel timing for the roofline (HIP events on the library stream) ----
+    ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
+    grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
+    ctx.leapfrog_end()
+    # algorithmic bytes per gradient launch: int8 genotypes read once
+    # (n * sum m_b), the per-branch f32 targets (4 n B) and the partial slabs
+    x_bytes = n * m_b * nb
+    y_bytes = 4 * n * nb
+    P = m_b * widths[0] + widths[0] * widths[1] + widths[1] + widths[0] + widths[1]
+    alg_bytes = x_bytes + y_bytes
+    achieved = alg_bytes / (grad_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        c = cpu_baseline(n, m_b, widths, args.cpu_sample_branches, args.cpu_sample_steps)
+        if c is not None:
+            cpu = {"value": c["branch_steps_per_s"] / B_total, "unit": "leapfrog steps/s",
+                   "cores": c["threads"], "kind": "port",
+                   "sample": f"{args.cpu_sample_branches} branches x {args.cpu_sample_steps} leapfrog steps at "
+                             f"n={n}, m_b={m_b}, widths={widths} (C restatement of the reference op order, f32, "
+                             f"X read 3x per step), extrapolated x{B_total}/{args.cpu_sample_branches} branches; "
+                             f"{c['seconds']:.1f}s of CPU work"}
+
+    steps_per_s = args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": steps_per_s,
+            "unit": "leapfrog steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int8 genotypes x f32 params (i8 MFMA digits, f32 accumulate)",
+            "data": "synthetic (device-generated Binomial(2,p) genotypes, random-init branches)",
+            "config": {"workload": f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W=S=4, "
+                                   "RidgeARD, tanh, Izmailov step sizes",
+                       "n": n, "snps": M_total, "branches": B_total, "layer_widths": widths,
+                       "branches_per_gpu": nb, "parallelism": f"branch-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_fused_grad", "kernel_ms": grad_ms, "alg_bytes_per_launch": alg_bytes,
+                         "packed_bytes_per_launch": ctx.packed_genotype_bytes, "update_kernel_ms": upd_ms},
+            "cpu_baseline": cpu,
+            "accept_rate": acc_all / nb_all,
+            "setup_s": setup_s,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -171,7 +171,17 @@ int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* num_accepted)
 /* device pointer to the branch predictions f_b(theta_L) written by the last
  * leapfrog step (indexed by branch id: pred[b*n + i]), for the residual update. */
 int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out);
+/* residual change of the finished trajectory, written to a DEVICE buffer of n
+ * floats: out[i] = sum over the session's accepted branches of
+ * f_b(theta_L)[i] - f_b(theta_0)[i]  (net.rs:279-300 bookkeeping: the caller
+ * does residual -= out, after an all-reduce over GPUs when branches are sharded) */
+int bann_leapfrog_residual_delta_device(bann_ctx* ctx, float* out_device);
 int bann_synchronize(bann_ctx* ctx);
+/* measurement hook: times `iters` packed gradient launches and `iters` update
+ * launches (gradient-only mode, no state change) of the active leapfrog
+ * session's branch set with HIP events on the context's stream; returns the
+ * average milliseconds per launch of each. */
+int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms);
 
 /* ---------------- introspection for tests / profiling ---------------- */
 /* which gradient kernel serves branch b: 1 = fused single-pass MFMA/VALU kernel,

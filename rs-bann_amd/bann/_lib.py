@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)                       # rs-bann_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "librsbann_amd.so")
+LIB_PATH = os.environ.get("BANN_LIB", os.path.join(PKG_ROOT, "librsbann_amd.so"))
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "bann.h")
 
 BANN_OK = 0
@@ -72,7 +72,9 @@ SIGNATURES = {
     "bann_leapfrog_steps": (C.c_int, [_P, _i32]),
     "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),
     "bann_leapfrog_predictions_device": (C.c_int, [_P, C.POINTER(_pf32)]),
+    "bann_leapfrog_residual_delta_device": (C.c_int, [_P, _P]),
     "bann_synchronize": (C.c_int, [_P]),
+    "bann_profile_session": (C.c_int, [_P, _i32, _pf32, _pf32]),
     "bann_branch_kernel_path": (C.c_int, [_P, _i32]),
     "bann_set_fused_enabled": (C.c_int, [_P, _i32]),
     "bann_packed_genotype_bytes": (_i64, [_P]),

@@ -224,10 +224,21 @@ class BannContext:
         self._check(self._lib.bann_leapfrog_end(self._h, _ptr(st, C.c_int32), C.byref(acc)))
         return st, acc.value
 
+    def residual_delta_device(self, out_ptr: int):
+        """write sum_{accepted b} f_b(theta_L) - f_b(theta_0) (n floats) to a device pointer."""
+        self._check(self._lib.bann_leapfrog_residual_delta_device(self._h, C.c_void_p(out_ptr)))
+
     def predictions_device_ptr(self) -> int:
         p = C.POINTER(C.c_float)()
         self._check(self._lib.bann_leapfrog_predictions_device(self._h, C.byref(p)))
         return C.cast(p, C.c_void_p).value or 0
+
+    def profile_session(self, iters: int = 5):
+        """(grad_ms, update_ms) average per launch, HIP events on the library stream."""
+        g = C.c_float()
+        u = C.c_float()
+        self._check(self._lib.bann_profile_session(self._h, iters, C.byref(g), C.byref(u)))
+        return g.value, u.value
 
     def synchronize(self):
         self._check(self._lib.bann_synchronize(self._h))

@@ -33,12 +33,12 @@ struct BranchHost {
 
 struct Plan {
   std::vector<int32_t> all, generic;
-  std::vector<GradItem> items[5];
-  int32_t nwaves[5] = {0, 0, 0, 0, 0};
+  std::vector<GradItem> items[BANN_NGROUPS];
+  int32_t nwaves[BANN_NGROUPS] = {};
   int32_t max_p_generic = 0, max_p = 0;
   int32_t* d_all = nullptr;
   int32_t* d_gen = nullptr;
-  GradItem* d_items[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  GradItem* d_items[BANN_NGROUPS] = {};
   bool owns = false;
 };
 
@@ -68,6 +68,7 @@ struct bann_ctx {
   float *d_theta = nullptr, *d_mom = nullptr, *d_eps = nullptr, *d_theta0 = nullptr, *d_lam = nullptr,
         *d_lamld = nullptr, *d_grad = nullptr, *d_part = nullptr;
   double* d_rss_part = nullptr;
+  float* d_pred0 = nullptr;
   float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
   double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
   int32_t *d_status = nullptr, *d_uturn = nullptr;
@@ -139,6 +140,7 @@ static void refresh_state(bann_ctx* ctx) {
   s.rss_part = ctx->d_rss_part;
   s.y = ctx->d_y;
   s.pred = ctx->d_pred;
+  s.pred0 = ctx->d_pred0;
   s.scr = ctx->d_scr;
   s.eprec = ctx->d_eprec;
   s.h0 = ctx->d_h0;
@@ -242,7 +244,7 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       p.max_p_generic = std::max(p.max_p_generic, h.P);
       continue;
     }
-    const int L = h.L;
+    const int grp = (h.L - 2) * 5 + h.act;
     const int64_t nfrag = ctx->nfrag;
     const int ns = h.dev.nsplits;
     for (int s = 0; s < ns; ++s) {
@@ -251,9 +253,9 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       it.split = s;
       it.frag_begin = (int32_t)(nfrag * s / ns);
       it.frag_end = (int32_t)(nfrag * (s + 1) / ns);
-      p.items[L].push_back(it);
+      p.items[grp].push_back(it);
     }
-    p.nwaves[L] = std::max(p.nwaves[L], h.dev.nchunks);
+    p.nwaves[grp] = std::max(p.nwaves[grp], h.dev.nchunks);
   }
   if (persistent) {
     p.owns = true;
@@ -263,10 +265,10 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
     if (!p.generic.empty())
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
-    for (int L = 2; L <= 4; ++L) {
-      if (p.items[L].empty()) continue;
-      CK(dalloc(&p.d_items[L], (int64_t)p.items[L].size()));
-      CK(hipMemcpyAsync(p.d_items[L], p.items[L].data(), p.items[L].size() * sizeof(GradItem),
+    for (int g = 0; g < BANN_NGROUPS; ++g) {
+      if (p.items[g].empty()) continue;
+      CK(dalloc(&p.d_items[g], (int64_t)p.items[g].size()));
+      CK(hipMemcpyAsync(p.d_items[g], p.items[g].data(), p.items[g].size() * sizeof(GradItem),
                         hipMemcpyHostToDevice, ctx->stream));
     }
   } else {
@@ -278,12 +280,12 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
     int64_t off = 0;
-    for (int L = 2; L <= 4; ++L) {
-      if (p.items[L].empty()) continue;
-      p.d_items[L] = ctx->d_items_scr + off;
-      CK(hipMemcpyAsync(p.d_items[L], p.items[L].data(), p.items[L].size() * sizeof(GradItem),
+    for (int g = 0; g < BANN_NGROUPS; ++g) {
+      if (p.items[g].empty()) continue;
+      p.d_items[g] = ctx->d_items_scr + off;
+      CK(hipMemcpyAsync(p.d_items[g], p.items[g].data(), p.items[g].size() * sizeof(GradItem),
                         hipMemcpyHostToDevice, ctx->stream));
-      off += (int64_t)p.items[L].size();
+      off += (int64_t)p.items[g].size();
     }
   }
   return BANN_OK;
@@ -291,10 +293,10 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 
 // gradient (partials) of every branch in the plan at the current theta
 static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
-  for (int L = 2; L <= 4; ++L)
-    if (!p.items[L].empty())
-      launch_fused_grad(ctx->st, p.d_items[L], (int32_t)p.items[L].size(), p.nwaves[L], L, write_pred,
-                        ctx->stream);
+  for (int g = 0; g < BANN_NGROUPS; ++g)
+    if (!p.items[g].empty())
+      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 5 + 2, g % 5,
+                        write_pred, ctx->stream);
   if (!p.generic.empty())
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
   CK(hipGetLastError());
@@ -339,7 +341,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
   free_plan(ctx->lf);
   void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_dig, ctx->d_fc, ctx->d_mub,
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
-                  ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_scr, ctx->d_eprec,
+                  ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
                   ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr};
   for (void* p : bufs) dfree(p);
@@ -542,7 +544,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   }
   int64_t target_items = 8192;
   if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
-  const int64_t frags_per_item = std::max<int64_t>(8, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
+  int64_t min_frags = 64;  // >= 16 tiles per work item amortises the per-item prologue/epilogue
+  if (const char* e = getenv("BANN_MIN_FRAGS")) min_frags = std::max<int64_t>(1, atoll(e));
+  const int64_t frags_per_item =
+      std::max<int64_t>(min_frags, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
   int64_t x_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
@@ -605,6 +610,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipMemsetAsync(ctx->d_y, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_pred, nb * n));
   CK(hipMemsetAsync(ctx->d_pred, 0, nb * n * sizeof(float), ctx->stream));
+  CK(dalloc(&ctx->d_pred0, nb * n));
+  CK(hipMemsetAsync(ctx->d_pred0, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_scr, scr_off));
   CK(dalloc(&ctx->d_eprec, nb));
   CK(dalloc(&ctx->d_u, nb));
@@ -896,8 +903,11 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
   if (rc) return rc;
   rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
   if (rc) return rc;
-  rc = run_grad(ctx, ctx->lf, 0);
+  rc = run_grad(ctx, ctx->lf, 1);
   if (rc) return rc;
+  for (int32_t b : ctx->lf.all)
+    CK(hipMemcpyAsync(ctx->d_pred0 + (int64_t)b * ctx->n, ctx->d_pred + (int64_t)b * ctx->n, ctx->n * sizeof(float),
+                      hipMemcpyDeviceToDevice, ctx->stream));
   launch_update(ctx->st, ctx->lf.d_all, nb, MODE_INIT, 0, ctx->stream);
   CK(hipGetLastError());
   ctx->lf_active = true;
@@ -940,8 +950,45 @@ extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* nu
   return BANN_OK;
 }
 
+extern "C" int bann_leapfrog_residual_delta_device(bann_ctx* ctx, float* out_device) {
+  if (!ctx || !out_device) return BANN_E_ARG;
+  if (ctx->lf.all.empty() || ctx->lf_active) return fail(ctx, BANN_E_STATE, "call after bann_leapfrog_end");
+  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), out_device, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
 extern "C" int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out) {
   if (!ctx || !out) return BANN_E_ARG;
   *out = ctx->d_pred;
+  return BANN_OK;
+}
+
+extern "C" int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms) {
+  if (!ctx || !ctx->lf_active) return fail(ctx, BANN_E_STATE, "no leapfrog session");
+  if (iters <= 0) return fail(ctx, BANN_E_ARG, "iters must be positive");
+  hipEvent_t e0, e1, e2;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventCreate(&e2));
+  const int32_t nb = (int32_t)ctx->lf.all.size();
+  CK(hipEventRecord(e0, ctx->stream));
+  for (int i = 0; i < iters; ++i) {
+    int rc = run_grad(ctx, ctx->lf, 0);
+    if (rc) return rc;
+  }
+  CK(hipEventRecord(e1, ctx->stream));
+  for (int i = 0; i < iters; ++i) launch_update(ctx->st, ctx->lf.d_all, nb, MODE_GRAD, 0, ctx->stream);
+  CK(hipEventRecord(e2, ctx->stream));
+  CK(hipEventSynchronize(e2));
+  float t01 = 0.f, t12 = 0.f;
+  CK(hipEventElapsedTime(&t01, e0, e1));
+  CK(hipEventElapsedTime(&t12, e1, e2));
+  if (grad_ms) *grad_ms = t01 / iters;
+  if (update_ms) *update_ms = t12 / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipEventDestroy(e2);
   return BANN_OK;
 }

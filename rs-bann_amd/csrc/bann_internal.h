@@ -73,6 +73,7 @@ struct DevState {
   double* rss_part;       // [nbranch][max splits]
   float* y;               // targets [nbranch][n]
   float* pred;            // predictions [nbranch][n]
+  float* pred0;           // predictions at the trajectory start
   float* scr;             // generic-path scratch
   float* eprec;           // error precision per branch
   double* h0;             // initial -H per branch
@@ -102,7 +103,8 @@ void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp
                          float* sig_b, hipStream_t s);
 
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
-                       int write_pred, hipStream_t s);
+                       int32_t act, int write_pred, hipStream_t s);
+#define BANN_NGROUPS 15  // fused launch groups: (L - 2) * 5 + activation, L in [2, 4]
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
@@ -110,3 +112,4 @@ void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int3
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
+void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s);

@@ -20,10 +20,20 @@
 //  * k_generic_*   — straightforward multi-pass kernels (any widths/depth),
 //    reference op order, f32 standardized inputs, double accumulation.
 #include "activations.h"
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "bann_internal.h"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+
+// Ablation switches for profiling builds only (make ABLATE=n): 1 = skip the head,
+// 2 = skip the VALU backward, 4 = skip the MFMA forward.  0 in every shipped build.
+#ifndef BANN_ABLATE
+#define BANN_ABLATE 0
+#endif
 
 // ===========================================================================
 // generic path
@@ -194,21 +204,30 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
-template <int NL, int NWMAX>
+// One work item = fragments [frag_begin, frag_end) of one branch.  Wave w owns
+// marker chunk w for the whole item: its A operand (W0/sigma digits) and its
+// dW0 accumulators stay in registers.  Per tile of 4 fragments (64
+// individuals): every wave streams its 4 x 1 KiB slab (prefetched one tile
+// ahead into a ping-pong register buffer; loads are branch-free so the counted
+// s_waitcnt keeps the next tile in flight), runs 4 MFMAs, publishes partial Z0
+// through LDS; wave 0 runs the head for the 64 individuals; every wave then
+// accumulates its dW0 block from the same genotype registers.
+template <int NL, int NWMAX, int ACT>
 __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const GradItem* __restrict__ items,
                                                            int write_pred) {
   constexpr int NH = NL - 1;  // layers with activations (0 .. L-2)
-  __shared__ float s_zp[NWMAX][BANN_TILE_FRAGS][16][4];  // per-chunk partial Z0
-  __shared__ v4f s_delta[BANN_TILE_FRAGS][16];           // delta0 of the tile
+  constexpr int T = BANN_TILE_FRAGS;
+  __shared__ float s_zp[NWMAX][T][16][4];  // per-chunk partial Z0
+  __shared__ v4f s_delta[T][16];           // delta0 of the tile
   __shared__ HeadLds s_hd;
   __shared__ float s_db0[4];
 
   const GradItem it = items[blockIdx.x];
   const BranchDev& bd = st.br[it.branch];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const int nch = bd.nchunks;
   const bool has_chunk = wave < nch;
-  const int act = bd.act;
   const int64_t n = st.n;
 
   // ---- head parameters into LDS (zero padded) ----
@@ -230,15 +249,16 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
       s_hd.bias[0][k] = (k < bd.widths[0]) ? st.fc[it.branch].c0[k] : 0.f;
     }
   }
-  float scale = 0.f;
-  v4i adig = {0, 0, 0, 0};
-  if (has_chunk) {
-    scale = st.fc[it.branch].scale[lane >> 4];
-    adig = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)wave * 64 + lane) * 16);
-  }
+  const int mych = has_chunk ? wave : nch - 1;  // chunk-less waves re-read a valid slab (never used)
+  const float scale = st.fc[it.branch].scale[lane >> 4];
+  const v4i adig = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)mych * 64 + lane) * 16);
   __syncthreads();
 
-  const int8_t* xb = st.xpk + bd.x_off;
+  const int64_t frag_bytes = (int64_t)nch * 1024;
+  const int8_t* xw = st.xpk + bd.x_off + ((int64_t)mych * 64 + lane) * 16;
+  const int fend = it.frag_end, flast = fend - 1;
+  const float* ybr = st.y + bd.y_off;
+
   float acc[16][4];
 #pragma unroll
   for (int j = 0; j < 16; ++j)
@@ -260,27 +280,27 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
       for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
   }
 
-  auto load_tile = [&](int f0, v4i (&xv)[BANN_TILE_FRAGS]) {
+  // branch-free loads: fragments past the item end are clamped to its last one
+  auto load_tile = [&](int f0, v4i (&xv)[T], float& yv) {
 #pragma unroll
-    for (int q = 0; q < BANN_TILE_FRAGS; ++q) {
-      const int f = f0 + q;
-      if (has_chunk && f < it.frag_end)
-        xv[q] = *reinterpret_cast<const v4i*>(xb + (((int64_t)f * nch + wave) * 64 + lane) * 16);
-      else
-        xv[q] = v4i{0, 0, 0, 0};
+    for (int q = 0; q < T; ++q) {
+      const int f = min(f0 + q, flast);
+      xv[q] = *reinterpret_cast<const v4i*>(xw + (int64_t)f * frag_bytes);
     }
+    const int64_t row = (int64_t)min(f0 + (lane >> 4), flast) * 16 + (lane & 15);
+    yv = ybr[row < n ? row : n - 1];
   };
 
-  v4i xcur[BANN_TILE_FRAGS], xnext[BANN_TILE_FRAGS];
-  load_tile(it.frag_begin, xcur);
-  for (int f0 = it.frag_begin; f0 < it.frag_end; f0 += BANN_TILE_FRAGS) {
-    if (f0 + BANN_TILE_FRAGS < it.frag_end) load_tile(f0 + BANN_TILE_FRAGS, xnext);
-
+  auto do_tile = [&](int f0, const v4i (&xv)[T], float yv) {
     // ---- forward, masked first layer on MFMA: partial Z0 of this chunk ----
     if (has_chunk) {
 #pragma unroll
-      for (int q = 0; q < BANN_TILE_FRAGS; ++q) {
-        v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig, xcur[q], v4i{0, 0, 0, 0}, 0, 0, 0);
+      for (int q = 0; q < T; ++q) {
+#if BANN_ABLATE & 4
+        v4i d = xv[q];
+#else
+        v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig, xv[q], v4i{0, 0, 0, 0}, 0, 0, 0);
+#endif
         // lane l: individual (l & 15), column k = l >> 4, digits d[0..3]
         const float zp = scale * ((float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f +
                                   (float)d[3] * 0x1p-21f);
@@ -294,17 +314,26 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
       const int q = lane >> 4, rr = lane & 15;
       const int f = f0 + q;
       const int64_t row = (int64_t)f * 16 + rr;
-      const bool valid = (f < it.frag_end) && (row < n);
+      const bool valid = (f < fend) && (row < n);
+#if BANN_ABLATE & 1
+      const v4f p0 = *reinterpret_cast<const v4f*>(&s_zp[0][q][rr][0]);
+      s_delta[q][rr] = p0 * 1e-3f;
+      (void)valid;
+      (void)yv;
+#else
       float z[NH][4], a[NH][4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) z[0][k] = s_hd.bias[0][k];
-      for (int w = 0; w < nch; ++w) {
-        const v4f p = *reinterpret_cast<const v4f*>(&s_zp[w][q][rr][0]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) z[0][k] += p[k];
+      for (int w = 0; w < NWMAX; ++w) {
+        if (w < nch) {
+          const v4f p = *reinterpret_cast<const v4f*>(&s_zp[w][q][rr][0]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) z[0][k] += p[k];
+        }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) a[0][k] = act_h(z[0][k], act);
+      for (int k = 0; k < 4; ++k) a[0][k] = act_h_t<ACT>(z[0][k]);
 #pragma unroll
       for (int l = 1; l < NH; ++l) {
 #pragma unroll
@@ -313,13 +342,13 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
 #pragma unroll
           for (int j = 0; j < 4; ++j) s = fmaf(a[l - 1][j], s_hd.W[l][j][k], s);
           z[l][k] = s;
-          a[l][k] = act_h(s, act);
+          a[l][k] = act_h_t<ACT>(s);
         }
       }
       float out = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], s_hd.W[NL - 1][j][0], out);
-      const float e = valid ? out - st.y[bd.y_off + row] : 0.f;
+      const float e = valid ? out - yv : 0.f;
       if (write_pred && valid) st.pred[bd.y_off + row] = out;
       rss += (double)e * (double)e;
       float err[4];
@@ -333,35 +362,45 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
         float d[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          d[k] = act_dh(z[l][k], a[l][k], act) * err[k];
+          d[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
           db[l][k] += d[k];
         }
         if (l >= 1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float s = 0.f;
+            float sj = 0.f;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               dW[l - 1][j][k] = fmaf(a[l - 1][j], d[k], dW[l - 1][j][k]);
-              s = fmaf(d[k], s_hd.W[l][j][k], s);
+              sj = fmaf(d[k], s_hd.W[l][j][k], sj);
             }
-            err[j] = s;
+            err[j] = sj;
           }
         } else {
           s_delta[q][rr] = v4f{d[0], d[1], d[2], d[3]};
         }
       }
+#endif
     }
     __syncthreads();
 
     // ---- backward, masked first layer on VALU: acc[j][k] += x_j * delta0_k ----
+#if BANN_ABLATE & 2
     if (has_chunk) {
 #pragma unroll
-      for (int q = 0; q < BANN_TILE_FRAGS; ++q) {
+      for (int q = 0; q < T; ++q) {
+        const v4f dl = s_delta[q][lane & 15];
+        asm volatile("" ::"v"(xv[q]), "v"(dl));
+      }
+    }
+#else
+    if (has_chunk) {
+#pragma unroll
+      for (int q = 0; q < T; ++q) {
         const v4f dl = s_delta[q][lane & 15];
 #pragma unroll
         for (int w4 = 0; w4 < 4; ++w4) {
-          const uint32_t word = (uint32_t)xcur[q][w4];
+          const uint32_t word = (uint32_t)xv[q][w4];
 #pragma unroll
           for (int bq = 0; bq < 4; ++bq) {
             const float x = (float)((word >> (8 * bq)) & 0xFFu);
@@ -371,8 +410,19 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
         }
       }
     }
-#pragma unroll
-    for (int q = 0; q < BANN_TILE_FRAGS; ++q) xcur[q] = xnext[q];
+#endif
+  };
+
+  v4i xa[T], xb[T];
+  float ya, yb;
+  load_tile(it.frag_begin, xa, ya);
+  for (int f0 = it.frag_begin;; f0 += 2 * T) {
+    load_tile(f0 + T, xb, yb);
+    do_tile(f0, xa, ya);
+    if (f0 + T >= fend) break;
+    load_tile(f0 + 2 * T, xa, ya);
+    do_tile(f0 + T, xb, yb);
+    if (f0 + 2 * T >= fend) break;
   }
 
   // ---- head sums: reduce over the 64 rows-lanes of wave 0 and publish ----
@@ -430,33 +480,422 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
     for (int j = 0; j < 16; ++j)
 #pragma unroll
       for (int k = 0; k < 4; ++k) mine[k] = (j == rr) ? acc[j][k] : mine[k];
-    const int s = wave * 64 + (lane >> 4) * 16 + rr;
-    if (s < bd.m) {
-      const float mu = st.mu[bd.mk_off + s], sg = st.sigma[bd.mk_off + s];
+    const int sidx = wave * 64 + (lane >> 4) * 16 + rr;
+    if (sidx < bd.m) {
+      const float mu = st.mu[bd.mk_off + sidx], sg = st.sigma[bd.mk_off + sidx];
       const int w0 = bd.widths[0];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (k < w0) part[bd.woff[0] + k * bd.m + s] = sg > 0.f ? (mine[k] - mu * s_db0[k]) / sg : 0.f;
+        if (k < w0) part[bd.woff[0] + k * bd.m + sidx] = sg > 0.f ? (mine[k] - mu * s_db0[k]) / sg : 0.f;
     }
   }
 }
 
-template <int NL>
-static void launch_fused_nl(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int wp,
-                            hipStream_t s) {
+#define LDS_BARRIER()                                      \
+  do {                                                     \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
+    __builtin_amdgcn_s_barrier();                          \
+    asm volatile("" ::: "memory");                         \
+  } while (0)
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// LDS stores issued through inline asm: hipcc's wait-count pass does not see
+// them, so it does not drain in-flight LDS-DMA (vmcnt(0)) in front of every
+// store as it does for a ds_write it cannot disambiguate from the DMA target.
+// Their completion is ordered by the explicit lgkmcnt(0) of LDS_BARRIER.
+__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
+// LDS-DMA through inline asm as well: the wave's own counted "s_waitcnt vmcnt"
+// (explicit, below) is then the only wait on it.  M0 = wave-uniform LDS base;
+// the data lands at M0 + 16 * lane (4 * lane for the dword form).
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");
+}
+__device__ __forceinline__ void lds_st_f32(float* p, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_st_v4f(v4f* p, v4f v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined variant (default): wave 0 is a dedicated HEAD wave, waves 1..NW own
+// the marker chunks.  One barrier per tile; in iteration t the chunk waves run
+// forward(t) and backward(t-1) while the head wave runs head(t-1)... precisely:
+//   chunk wave, iteration t:  DMA X(t+D) -> wait X(t) -> MFMA fwd(t) -> zp[t&1]
+//                              BARRIER(t)
+//                              bwd(t-1) with delta[(t-1)&1] and X(t-1) (LDS ring)
+//   head wave,  iteration t:  BARRIER(t) -> head(t) from zp[t&1] -> delta[t&1]
+// so the latency-bound per-individual head overlaps the chunk waves' streaming
+// MFMA/VALU work instead of stalling them, and the head's registers and the
+// chunk waves' dW0 accumulators are never live in the same wave.
+// ---------------------------------------------------------------------------
+template <int NL, int NWMAX, int ACT, int R>
+__global__ void __launch_bounds__(64 * (NWMAX + 1))
+    k_fused_grad_pipe(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  static_assert(R == 3, "the slot-unrolled loops below assume a 3-slot ring");
+  constexpr int NH = NL - 1;
+  constexpr int T = BANN_TILE_FRAGS;
+  constexpr int D = R - 2;  // prefetch distance in tiles
+  constexpr int SLAB = 1024;
+  // Every LDS-DMA target is its OWN __shared__ object and every slot index is a
+  // compile-time constant: hipcc can then prove that a ds_read of slot s does
+  // not alias the DMA in flight into slot s+D and keeps the counted vmcnt wait
+  // (with one shared array it drains the prefetch with vmcnt(0) before every read).
+  __shared__ __attribute__((aligned(16))) char xr0[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) char xr1[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) char xr2[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) float yr0[64];
+  __shared__ __attribute__((aligned(16))) float yr1[64];
+  __shared__ __attribute__((aligned(16))) float yr2[64];
+  __shared__ __attribute__((aligned(16))) float s_zp[2][NWMAX][T][16][4];
+  __shared__ __attribute__((aligned(16))) v4f s_delta[2][T][16];
+  __shared__ __attribute__((aligned(16))) HeadLds s_hd;
+  __shared__ __attribute__((aligned(16))) float s_db0[4];
+
+  const GradItem it = items[blockIdx.x];
+  const BranchDev& bd = st.br[it.branch];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = bd.nchunks;
+  const int64_t n = st.n;
+  const int fbeg = it.frag_begin, fend = it.frag_end, flast = fend - 1;
+  const int ntiles = (fend - fbeg + T - 1) / T;
+
+  for (int t = threadIdx.x; t < BANN_MAXL * 20; t += blockDim.x) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (l >= 1 && l < NL) {
+      if (r < 16) {
+        const int j = r >> 2, k = r & 3;
+        if (j < bd.win[l] && k < bd.widths[l]) v = st.theta[bd.p_off + bd.woff[l] + k * bd.win[l] + j];
+        s_hd.W[l][j][k] = v;
+      } else {
+        const int k = r - 16;
+        if (l < NL - 1 && k < bd.widths[l]) v = st.theta[bd.p_off + bd.boff[l] + k];
+        s_hd.bias[l][k] = v;
+      }
+    } else if (l == 0 && r >= 16) {
+      const int k = r - 16;
+      s_hd.bias[0][k] = (k < bd.widths[0]) ? st.fc[it.branch].c0[k] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+
+  if (wave == 0) {
+    // ===================== head wave =====================
+    const int64_t y_off = bd.y_off;
+    const float* ybr = st.y + y_off;
+    float* predb = st.pred + y_off;
+    auto yslot = [&](auto sc) -> float* {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) return yr0;
+      else if constexpr (s == 1) return yr1;
+      else return yr2;
+    };
+    auto issue_y = [&](int t, auto sc) {
+      const int64_t row = (int64_t)min(fbeg + t * T + (lane >> 4), flast) * 16 + (lane & 15);
+      glds4(ybr + (row < n ? row : n - 1), yslot(sc));
+    };
+    double rss = 0.0;
+    float db[NH][4], dWo[4];
+    float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dWo[k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+    }
+    issue_y(0, std::integral_constant<int, 0>{});
+    // iteration t uses y slot t % 3 and zp / delta buffer t & 1
+    auto head_iter = [&](int t, auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (t < ntiles) issue_y(t + D, std::integral_constant<int, (s + D) % R>{});
+      LDS_BARRIER();
+      if (t == ntiles) return;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");  // y(t) landed (y(t+D) may fly)
+      const int q = lane >> 4, rr = lane & 15;
+      const int f = fbeg + t * T + q;
+      const int64_t row = (int64_t)f * 16 + rr;
+      const bool valid = (f < fend) && (row < n);
+      const float yv = yslot(sc)[lane];
+      const int zb = t & 1;
+#if BANN_ABLATE & 1
+      {
+        const v4f p0 = *reinterpret_cast<const v4f*>(&s_zp[zb][0][q][rr][0]);
+        lds_st_v4f(&s_delta[zb][q][rr], p0 * 1e-3f);
+        (void)valid;
+        (void)yv;
+      }
+#else
+      float z[NH][4], a[NH][4];
+      v4f zs = *reinterpret_cast<const v4f*>(&s_hd.bias[0][0]);
+#pragma unroll
+      for (int w = 0; w < NWMAX; ++w) {
+        const v4f p = *reinterpret_cast<const v4f*>(&s_zp[zb][w][q][rr][0]);  // chunk-less waves wrote 0
+        zs += p;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[0][k] = zs[k];
+        a[0][k] = act_h_t<ACT>(z[0][k]);
+      }
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float sacc = s_hd.bias[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc = fmaf(a[l - 1][j], s_hd.W[l][j][k], sacc);
+          z[l][k] = sacc;
+          a[l][k] = act_h_t<ACT>(sacc);
+        }
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], s_hd.W[NL - 1][j][0], out);
+      const float e = valid ? out - yv : 0.f;
+      if (write_pred && valid) predb[row] = out;
+      rss += (double)e * (double)e;
+      float err[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+        err[j] = e * s_hd.W[NL - 1][j][0];
+      }
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        float d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
+          db[l][k] += d[k];
+        }
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float sj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dW[l - 1][j][k] = fmaf(a[l - 1][j], d[k], dW[l - 1][j][k]);
+              sj = fmaf(d[k], s_hd.W[l][j][k], sj);
+            }
+            err[j] = sj;
+          }
+        } else {
+          lds_st_v4f(&s_delta[zb][q][rr], v4f{d[0], d[1], d[2], d[3]});
+        }
+      }
+#endif
+    };
+    for (int t = 0; t <= ntiles; t += 3) {
+      head_iter(t, std::integral_constant<int, 0>{});
+      if (t + 1 > ntiles) break;
+      head_iter(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 > ntiles) break;
+      head_iter(t + 2, std::integral_constant<int, 2>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double rs = wave_sum_d(rss);
+    float db0s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db0s[k] = wave_sum(db[0][k]);
+    if (lane == 0) {
+      st.rss_part[(int64_t)it.branch * st.max_splits + it.split] = rs;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s_db0[k] = db0s[k];
+        if (k < bd.widths[0]) part[bd.boff[0] + k] = db0s[k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = wave_sum(dWo[j]);
+      if (lane == 0 && j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = wave_sum(db[l][k]);
+        if (lane == 0 && k < bd.widths[l]) part[bd.boff[l] + k] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float w = wave_sum(dW[l - 1][j][k]);
+          if (lane == 0 && j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = w;
+        }
+      }
+    }
+    __syncthreads();  // s_db0 visible to the chunk waves
+  } else {
+    // ===================== chunk waves =====================
+    const int cw = wave - 1;
+    const bool has_chunk = cw < nch;
+    const int mych = has_chunk ? cw : nch - 1;
+    float scale = has_chunk ? st.fc[it.branch].scale[lane >> 4] : 0.f;  // chunk-less: zp = 0
+    v4i adig = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)mych * 64 + lane) * 16);
+    // retire these loads now and hide their provenance, so the compiler's wait
+    // model does not re-wait on them (with vmcnt(0)) while the asm DMAs fly
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(adig), "+v"(scale));
+    const int64_t frag_bytes = (int64_t)nch * 1024;
+    const int8_t* xw = st.xpk + bd.x_off + ((int64_t)mych * 64 + lane) * 16;
+    auto xslot = [&](auto sc) -> char* {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) return xr0 + cw * T * SLAB;
+      else if constexpr (s == 1) return xr1 + cw * T * SLAB;
+      else return xr2 + cw * T * SLAB;
+    };
+    auto issue_x = [&](int t, auto sc) {
+      char* base = xslot(sc);
+#pragma unroll
+      for (int q = 0; q < T; ++q) {
+        const int f = min(fbeg + t * T + q, flast);
+        glds16(xw + (int64_t)f * frag_bytes, base + q * SLAB);
+      }
+    };
+    float acc[16][4];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[j][k] = 0.f;
+    issue_x(0, std::integral_constant<int, 0>{});
+    auto chunk_iter = [&](int t, auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (t < ntiles) {
+        issue_x(t + D, std::integral_constant<int, (s + D) % R>{});  // clamped: always valid
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T * D) : "memory");  // X(t) landed, X(t+D) in flight
+        const v4i* xs = reinterpret_cast<const v4i*>(xslot(sc)) + lane;
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          const v4i xv = xs[q * 64];
+#if BANN_ABLATE & 4
+          v4i d = xv;
+#else
+          v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig, xv, v4i{0, 0, 0, 0}, 0, 0, 0);
+#endif
+          const float zp = scale * ((float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f +
+                                    (float)d[3] * 0x1p-21f);
+          lds_st_f32(&s_zp[t & 1][cw][q][lane & 15][lane >> 4], zp);
+        }
+      }
+      LDS_BARRIER();
+      if (t >= 1 && has_chunk) {
+        const int tb = t - 1;
+        const v4i* xs = reinterpret_cast<const v4i*>(xslot(std::integral_constant<int, (s + R - 1) % R>{})) + lane;
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          const v4f dl = s_delta[tb & 1][q][lane & 15];
+          const v4i xv = xs[q * 64];
+#if BANN_ABLATE & 2
+          asm volatile("" ::"v"(xv), "v"(dl));
+#else
+#pragma unroll
+          for (int w4 = 0; w4 < 4; ++w4) {
+            const uint32_t word = (uint32_t)xv[w4];
+#pragma unroll
+            for (int bq = 0; bq < 4; ++bq) {
+              const float x = (float)((word >> (8 * bq)) & 0xFFu);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) acc[w4 * 4 + bq][k] = fmaf(x, dl[k], acc[w4 * 4 + bq][k]);
+            }
+          }
+#endif
+        }
+      }
+    };
+    for (int t = 0; t <= ntiles; t += 3) {
+      chunk_iter(t, std::integral_constant<int, 0>{});
+      if (t + 1 > ntiles) break;
+      chunk_iter(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 > ntiles) break;
+      chunk_iter(t + 2, std::integral_constant<int, 2>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // s_db0 published by the head wave
+    if (has_chunk) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float v = acc[j][k];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          acc[j][k] = v;
+        }
+      const int rr = lane & 15;
+      float mine[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mine[k] = (j == rr) ? acc[j][k] : mine[k];
+      const int sidx = cw * 64 + (lane >> 4) * 16 + rr;
+      if (sidx < bd.m) {
+        const float mu = st.mu[bd.mk_off + sidx], sg = st.sigma[bd.mk_off + sidx];
+        const int w0 = bd.widths[0];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < w0) part[bd.woff[0] + k * bd.m + sidx] = sg > 0.f ? (mine[k] - mu * s_db0[k]) / sg : 0.f;
+      }
+    }
+  }
+}
+
+// BANN_FUSED_VARIANT: "reg" (default, register-staged lockstep kernel) or "pipe"
+static int fused_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("BANN_FUSED_VARIANT");
+    v = (e && e[0] == 'p') ? 2 : 0;
+  }
+  return v;
+}
+
+template <int NL, int ACT>
+static void launch_fused_t(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int wp,
+                           hipStream_t s) {
+  if (fused_variant() == 2 && nwaves <= 8) {  // > 8 chunks: the LDS ring would not fit; use the reg kernel
+    hipLaunchKernelGGL((k_fused_grad_pipe<NL, 8, ACT, 3>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
+    return;
+  }
   if (nwaves <= 8)
-    hipLaunchKernelGGL((k_fused_grad<NL, 8>), dim3(nitems), dim3(64 * nwaves), 0, s, st, items, wp);
+    hipLaunchKernelGGL((k_fused_grad<NL, 8, ACT>), dim3(nitems), dim3(64 * nwaves), 0, s, st, items, wp);
   else
-    hipLaunchKernelGGL((k_fused_grad<NL, 16>), dim3(nitems), dim3(64 * nwaves), 0, s, st, items, wp);
+    hipLaunchKernelGGL((k_fused_grad<NL, 16, ACT>), dim3(nitems), dim3(64 * nwaves), 0, s, st, items, wp);
+}
+
+template <int NL>
+static void launch_fused_nl(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int act,
+                            int wp, hipStream_t s) {
+  switch (act) {
+    case 0: launch_fused_t<NL, 0>(st, items, nitems, nwaves, wp, s); break;
+    case 1: launch_fused_t<NL, 1>(st, items, nitems, nwaves, wp, s); break;
+    case 2: launch_fused_t<NL, 2>(st, items, nitems, nwaves, wp, s); break;
+    case 3: launch_fused_t<NL, 3>(st, items, nitems, nwaves, wp, s); break;
+    default: launch_fused_t<NL, 4>(st, items, nitems, nwaves, wp, s); break;
+  }
 }
 
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
-                       int write_pred, hipStream_t s) {
+                       int32_t act, int write_pred, hipStream_t s) {
   if (nitems <= 0) return;
   switch (L) {
-    case 2: launch_fused_nl<2>(st, items, nitems, nwaves, write_pred, s); break;
-    case 3: launch_fused_nl<3>(st, items, nitems, nwaves, write_pred, s); break;
-    case 4: launch_fused_nl<4>(st, items, nitems, nwaves, write_pred, s); break;
+    case 2: launch_fused_nl<2>(st, items, nitems, nwaves, act, write_pred, s); break;
+    case 3: launch_fused_nl<3>(st, items, nitems, nwaves, act, write_pred, s); break;
+    case 4: launch_fused_nl<4>(st, items, nitems, nwaves, act, write_pred, s); break;
     default: break;
   }
 }

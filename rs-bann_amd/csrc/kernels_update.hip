@@ -252,3 +252,22 @@ void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t
   const int pairs = (max_p + 1) / 2;
   hipLaunchKernelGGL(k_sample_momentum, dim3((pairs + 255) / 256, nb), dim3(256), 0, s, st, branches, seed);
 }
+
+// residual change of a finished trajectory (net.rs:292-300): accepted branches
+// replace their previous prediction by f(theta_L); rejected ones leave it.
+__global__ void k_residual_delta(DevState st, const int32_t* __restrict__ blist, int nb, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= st.n) return;
+  float acc = 0.f;
+  for (int q = 0; q < nb; ++q) {
+    const int b = blist[q];
+    if (st.status[b] != ST_ACCEPTED) continue;
+    const int64_t o = (int64_t)b * st.n + i;
+    acc += st.pred[o] - st.pred0[o];
+  }
+  out[i] = acc;
+}
+
+void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_residual_delta, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, st, branches, nb, out);
+}

@@ -1,0 +1,35 @@
+"""Kernel micro-benchmark: time the packed gradient launch (and the update
+launch) for a synthetic C3-like branch set.  Library chosen by BANN_LIB.
+  python tools/kbench.py --branches 250 --n 50000 --m 500"""
+import argparse, json, math, os, sys, time
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rs-bann_amd"))
+from bann import BannContext
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--branches", type=int, default=250)
+ap.add_argument("--n", type=int, default=50000)
+ap.add_argument("--m", type=int, default=500)
+ap.add_argument("--widths", default="4,4,1")
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--tag", default="")
+a = ap.parse_args()
+w = [int(x) for x in a.widths.split(",")]
+ctx = BannContext(0)
+ctx.synthetic_genotypes(a.n, a.branches * a.m, seed=5)
+for b in range(a.branches):
+    ctx.add_branch(np.arange(b * a.m, (b + 1) * a.m), w, "tanh", "ridge_ard")
+ctx.finalize(free_raw=True)
+rng = np.random.default_rng(0)
+for b in range(a.branches):
+    P = ctx.num_params(b)
+    ctx.set_params(b, rng.normal(0, 1 / math.sqrt(a.m), P))
+    ctx.set_precisions(b, np.ones(ctx.num_precisions(b)))
+    ctx.set_target(b, rng.normal(size=a.n))
+ctx.leapfrog_begin(list(range(a.branches)), 2, 10.0, "izmailov", 0.1, seed=1)
+ctx.profile_session(2)
+g, u = ctx.profile_session(a.iters)
+xb = a.n * a.m * a.branches
+print(json.dumps(dict(tag=a.tag, lib=os.environ.get("BANN_LIB", "default"), grad_ms=g, update_ms=u,
+                      x_GBps=xb / g / 1e6, alg_GBps=(xb + 4 * a.n * a.branches) / g / 1e6)))
