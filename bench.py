@@ -4,8 +4,12 @@
 
 One "step" = one full-cohort leapfrog step: a packed gradient evaluation of
 every branch (one fused HIP launch) + the fused momentum/position/-H update
-(one launch).  Genotypes are synthetic (generated on the device), resident in
-HBM as int8 before the timed region.
+(one launch).  The timed region is one whole HMC trajectory of K steps for
+every branch: momentum draw + initial gradient, the K steps, the Metropolis
+decision and the residual change of the accepted branches (the bookkeeping of
+net.rs:279-300); value = K / elapsed.  Warmup = one untimed trajectory of W
+steps.  Genotypes are synthetic (generated on the device), resident in HBM as
+int8 before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W]
   (N > 1: launched by torch.distributed.run, one rank per GPU; the 1k branches
@@ -16,6 +20,7 @@ Prints ONE JSON line (rank 0).
 """
 import argparse
 import ctypes
+import glob
 import json
 import math
 import os
@@ -84,8 +89,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--step-factor", type=float, default=0.5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-branches", type=int, default=16)
-    ap.add_argument("--cpu-sample-steps", type=int, default=3)
+    ap.add_argument("--cpu-sample-branches", type=int, default=96)
+    ap.add_argument("--cpu-sample-steps", type=int, default=16)
     ap.add_argument("--profile-iters", type=int, default=10)
     args = ap.parse_args()
 
@@ -106,7 +111,6 @@ def main():
     m_b = M_total // B_total
     b0, b1 = rank * B_total // world, (rank + 1) * B_total // world
     nb = b1 - b0
-    L = args.warmup + args.steps
 
     t_setup = time.time()
     ctx = BannContext(local_rank)
@@ -136,11 +140,8 @@ def main():
         prec[len(widths) - 1] = np.array([out_prec])
         ctx.set_params(k, params[k])
         ctx.set_precisions(k, np.concatenate(prec).astype(np.float32))
-    preds = []
-    for k in range(nb):
-        p = ctx.predict(k)
-        preds.append(p)
-        fsum += p
+    preds = ctx.predict_many(list(range(nb)))   # one packed launch
+    fsum += preds.sum(axis=0, dtype=np.float64)
     if dist is not None:
         import torch
         tt = torch.tensor(fsum, device="cuda")
@@ -155,29 +156,37 @@ def main():
     ctx.synchronize()
     setup_s = time.time() - t_setup
 
-    import torch
     delta = None
-    if torch.cuda.is_available():   # initialise torch/HIP state before the timed region
+    if dist is not None:   # initialise torch/HIP state before the timed region
+        import torch
         delta = torch.zeros(n, dtype=torch.float32, device=f"cuda:{local_rank}")
         torch.cuda.synchronize()
     branches = list(range(nb))
-    ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=11 + rank)
+
+    def trajectory(L, seed):
+        """one HMC trajectory of L leapfrog steps for every branch of this rank:
+        momentum draw + initial gradient, L fused steps, Metropolis, and the
+        residual change of the accepted branches (all-reduced over ranks)."""
+        ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
+        ctx.leapfrog_steps(L)
+        status, acc = ctx.leapfrog_end()
+        if dist is not None:
+            ctx.residual_delta_device(delta.data_ptr())
+            dist.all_reduce(delta)
+            torch.cuda.synchronize()
+        else:   # one GPU: no torch in the process (rocprofv3 + torch's HIP runtime do not mix here)
+            ctx.residual_delta()
+        return acc
+
+    # warmup: a full trajectory of W steps (loads every kernel, ramps the clocks)
     if args.warmup:
-        ctx.leapfrog_steps(args.warmup)
+        trajectory(args.warmup, seed=7 + rank)
     ctx.synchronize()
     if dist is not None:
-        import torch
         torch.cuda.synchronize()
         dist.barrier()
     t0 = time.perf_counter()
-    ctx.leapfrog_steps(args.steps)
-    status, acc = ctx.leapfrog_end()          # final half step + Metropolis (device)
-    # residual update of the sweep: all-reduce of the n-vector over ranks (RCCL)
-    if delta is not None:
-        ctx.residual_delta_device(delta.data_ptr())
-        if dist is not None:
-            dist.all_reduce(delta)
-        torch.cuda.synchronize()
+    acc = trajectory(args.steps, seed=11 + rank)   # timed: one whole trajectory of K steps
     ctx.synchronize()
     if dist is not None:
         dist.barrier()
@@ -192,6 +201,9 @@ def main():
     else:
         acc_all, nb_all = float(acc), float(nb)
 
+    workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W=S=4, RidgeARD, tanh, "
+                "Izmailov step sizes")
+    kernel_name = ctx.fused_kernel_name()
     # ---- kernel timing for the roofline (HIP events on the library stream) ----
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
     grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
@@ -200,9 +212,17 @@ def main():
     # (n * sum m_b), the per-branch f32 targets (4 n B) and the partial slabs
     x_bytes = n * m_b * nb
     y_bytes = 4 * n * nb
-    P = m_b * widths[0] + widths[0] * widths[1] + widths[1] + widths[0] + widths[1]
     alg_bytes = x_bytes + y_bytes
     achieved = alg_bytes / (grad_ms * 1e-3) / 1e9
+
+    # HBM traffic per gradient launch, from the committed PMC pass of the same
+    # workload (tools/profile_round.sh; a --pmc run cannot time itself)
+    traffic, traffic_src = None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        pm = json.load(open(f))
+        if pm.get("config") == workload and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
+            traffic, traffic_src = pm["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+            break
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -230,13 +250,13 @@ def main():
             "vs_baseline": None,
             "dtype": "int8 genotypes x f32 params (i8 MFMA digits, f32 accumulate)",
             "data": "synthetic (device-generated Binomial(2,p) genotypes, random-init branches)",
-            "config": {"workload": f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W=S=4, "
-                                   "RidgeARD, tanh, Izmailov step sizes",
+            "config": {"workload": workload,
                        "n": n, "snps": M_total, "branches": B_total, "layer_widths": widths,
                        "branches_per_gpu": nb, "parallelism": f"branch-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_fused_grad", "kernel_ms": grad_ms, "alg_bytes_per_launch": alg_bytes,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                         "kernel": kernel_name, "kernel_ms": grad_ms, "alg_bytes_per_launch": alg_bytes,
                          "packed_bytes_per_launch": ctx.packed_genotype_bytes, "update_kernel_ms": upd_ms},
             "cpu_baseline": cpu,
             "accept_rate": acc_all / nb_all,

@@ -115,6 +115,9 @@ int bann_branch_get_params(bann_ctx* ctx, int32_t b, float* param_vec_out);
 /* BranchPrecisions::from_host (params.rs:248-262) */
 int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float* precision_vec);
 int bann_branch_get_precisions(bann_ctx* ctx, int32_t b, float* precision_vec_out);
+/* step sizes of branch b used by the last trajectory (hmc_step / leapfrog_begin),
+ * param_vec order (izmailov_step_sizes ridge_ard.rs:70-117 etc.) */
+int bann_branch_get_step_sizes(bann_ctx* ctx, int32_t b, float* out);
 /* target y_b (n floats) the branch is fitted to: the partial residual
  * residual + f_b(theta) of net.rs:279-280 */
 int bann_branch_set_target(bann_ctx* ctx, int32_t b, const float* y);
@@ -123,6 +126,10 @@ int bann_set_target_all(bann_ctx* ctx, const float* y);
 /* ---------------- per-branch math: replaces the BranchSampler methods ---------------- */
 /* predict (branch_sampler.rs:915-918, forward_feed 743-782): pred_out[n] */
 int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out);
+/* predictions of several branches from ONE packed gradient launch (the
+ * per-branch loop of net.rs:272-282 when the residual is rebuilt); pred_out is
+ * nb x n, row i = branch branches[i]. */
+int bann_predict_many(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* pred_out);
 /* rss (branch_sampler.rs:905-909) against the branch target */
 int bann_rss(bann_ctx* ctx, int32_t b, double* rss_out);
 /* log_density_gradient (branch_sampler.rs:380-391: backpropagate 813-875 +
@@ -176,6 +183,8 @@ int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out);
  * f_b(theta_L)[i] - f_b(theta_0)[i]  (net.rs:279-300 bookkeeping: the caller
  * does residual -= out, after an all-reduce over GPUs when branches are sharded) */
 int bann_leapfrog_residual_delta_device(bann_ctx* ctx, float* out_device);
+/* same, copied to a HOST buffer of n floats (device scratch owned by the context) */
+int bann_leapfrog_residual_delta(bann_ctx* ctx, float* out_host);
 int bann_synchronize(bann_ctx* ctx);
 /* measurement hook: times `iters` packed gradient launches and `iters` update
  * launches (gradient-only mode, no state change) of the active leapfrog
@@ -187,6 +196,8 @@ int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* up
 /* which gradient kernel serves branch b: 1 = fused single-pass MFMA/VALU kernel,
  * 0 = generic multi-pass kernels */
 int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
+/* name of the fused gradient kernel family used for branches of <= 512 markers */
+const char* bann_fused_kernel_name(void);
 /* force every branch onto the generic path (0) or allow the fused path (1) */
 int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
 /* bytes of packed genotype data read per full gradient evaluation of all branches */

@@ -73,6 +73,10 @@ SIGNATURES = {
     "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),
     "bann_leapfrog_predictions_device": (C.c_int, [_P, C.POINTER(_pf32)]),
     "bann_leapfrog_residual_delta_device": (C.c_int, [_P, _P]),
+    "bann_leapfrog_residual_delta": (C.c_int, [_P, _P]),
+    "bann_fused_kernel_name": (C.c_char_p, []),
+    "bann_branch_get_step_sizes": (C.c_int, [_P, C.c_int32, _P]),
+    "bann_predict_many": (C.c_int, [_P, _P, C.c_int32, _P]),
     "bann_synchronize": (C.c_int, [_P]),
     "bann_profile_session": (C.c_int, [_P, _i32, _pf32, _pf32]),
     "bann_branch_kernel_path": (C.c_int, [_P, _i32]),

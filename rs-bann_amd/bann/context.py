@@ -122,6 +122,9 @@ class BannContext:
     def kernel_path(self, b: int) -> str:
         return "fused" if self._check(self._lib.bann_branch_kernel_path(self._h, b)) == 1 else "generic"
 
+    def fused_kernel_name(self) -> str:
+        return self._lib.bann_fused_kernel_name().decode()
+
     @property
     def packed_genotype_bytes(self) -> int:
         return int(self._lib.bann_packed_genotype_bytes(self._h))
@@ -160,6 +163,18 @@ class BannContext:
     def predict(self, b: int) -> np.ndarray:
         out = np.zeros(self.n, np.float32)
         self._check(self._lib.bann_predict(self._h, b, _ptr(out, C.c_float)))
+        return out
+
+    def get_step_sizes(self, b: int) -> np.ndarray:
+        out = np.zeros(self.num_params(b), np.float32)
+        self._check(self._lib.bann_branch_get_step_sizes(self._h, b, _ptr(out, C.c_float)))
+        return out
+
+    def predict_many(self, branches) -> np.ndarray:
+        """(len(branches), n) predictions from one packed launch."""
+        bl = np.ascontiguousarray(branches, dtype=np.int32)
+        out = np.zeros((bl.size, self.n), np.float32)
+        self._check(self._lib.bann_predict_many(self._h, _ptr(bl, C.c_int32), bl.size, _ptr(out, C.c_float)))
         return out
 
     def rss(self, b: int) -> float:
@@ -227,6 +242,12 @@ class BannContext:
     def residual_delta_device(self, out_ptr: int):
         """write sum_{accepted b} f_b(theta_L) - f_b(theta_0) (n floats) to a device pointer."""
         self._check(self._lib.bann_leapfrog_residual_delta_device(self._h, C.c_void_p(out_ptr)))
+
+    def residual_delta(self) -> np.ndarray:
+        """sum_{accepted b} f_b(theta_L) - f_b(theta_0) as a host array of n floats."""
+        out = np.zeros(self.n, np.float32)
+        self._check(self._lib.bann_leapfrog_residual_delta(self._h, _ptr(out, C.c_float)))
+        return out
 
     def predictions_device_ptr(self) -> int:
         p = C.POINTER(C.c_float)()

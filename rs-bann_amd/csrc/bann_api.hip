@@ -69,6 +69,11 @@ struct bann_ctx {
         *d_lamld = nullptr, *d_grad = nullptr, *d_part = nullptr;
   double* d_rss_part = nullptr;
   float* d_pred0 = nullptr;
+  double* d_stepbase = nullptr;  // per-parameter Izmailov step base (sign: factor applies)
+  float* d_delta = nullptr;       // n floats: residual change of the last trajectory (host-copy variant)
+  float* d_delta_part = nullptr;  // per-branch-slice partial rows of the residual change
+  int32_t* h_status = nullptr;    // pinned host mirrors (trajectory status, residual change)
+  float* h_delta = nullptr;
   float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
   double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
   int32_t *d_status = nullptr, *d_uturn = nullptr;
@@ -190,22 +195,28 @@ static void expand_precisions(const BranchHost& h, std::vector<float>& lam, std:
   eprec = h.prec.back();
 }
 
-// step sizes in param_vec order (izmailov_step_sizes ridge_ard.rs:70-117, ridge_base.rs:83-114,
-// lasso_ard.rs:77-117, lasso_base.rs:83-114, std_normal_branch.rs:83-114; uniform 706-732;
-// random 654-681)
-static void host_step_sizes(const BranchHost& h, int mode, float c, int lint, std::mt19937_64& rng,
-                            std::vector<float>& eps) {
-  const BranchDev& d = h.dev;
+// random step sizes (branch_sampler.rs:654-681): U(0,1) * P^(-1/4) * c, drawn on
+// the host; uniform (706-732) and Izmailov (ridge_ard.rs:70-117, ridge_base.rs:
+// 83-114, lasso_ard.rs:77-117, lasso_base.rs:83-114, std_normal_branch.rs:83-114)
+// are formed on the device from step_bases below.
+static void host_random_step_sizes(const BranchHost& h, float c, std::mt19937_64& rng, std::vector<float>& eps) {
   eps.assign(h.P, c);
-  if (mode == BANN_STEP_UNIFORM) return;
-  if (mode == BANN_STEP_RANDOM) {
-    std::uniform_real_distribution<float> U(0.f, 1.f);
-    const float f = powf((float)h.P, -0.25f) * c;
-    for (auto& e : eps) e = U(rng) * f;
-    return;
-  }
+  std::uniform_real_distribution<float> U(0.f, 1.f);
+  const float f = powf((float)h.P, -0.25f) * c;
+  for (auto& e : eps) e = U(rng) * f;
+}
+
+// per-parameter Izmailov step base, so the device can form eps = base * c / L
+// for any factor c and trajectory length L without a host round trip:
+// ridge / bias terms pi / (2 sqrt(lam)), lasso 1 / (4 lam); negative = the
+// factor c does not apply (std_normal weights and biases).  eps = base * c / L
+// reproduces the reference's c * pi / (2 sqrt(lam) L) and c / (4 lam L).
+static void step_bases(const BranchHost& h, std::vector<double>& out) {
+  const BranchDev& d = h.dev;
+  out.assign(h.P, 0.0);
   const bool ard = (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD);
   const bool lasso = (h.prior == BANN_LASSO_ARD || h.prior == BANN_LASSO_BASE);
+  const bool stdn = h.prior == BANN_STD_NORMAL;
   const double PI = 3.14159265358979323846;
   int pi = 0;
   for (int l = 0; l < h.L; ++l) {
@@ -214,20 +225,20 @@ static void host_step_sizes(const BranchHost& h, int mode, float c, int lint, st
       for (int j = 0; j < wi; ++j) {
         const double lam = (ard && l < h.L - 1) ? h.prec[pi + j] : h.prec[pi];
         double e;
-        if (h.prior == BANN_STD_NORMAL)
-          e = PI / (2.0 * sqrt(lam) * lint);
+        if (stdn)
+          e = -PI / (2.0 * sqrt(lam));
         else if (lasso)
-          e = c / (4.0 * lam * lint);
+          e = 1.0 / (4.0 * lam);
         else
-          e = c * PI / (2.0 * sqrt(lam) * lint);
-        eps[d.woff[l] + k * wi + j] = (float)e;
+          e = PI / (2.0 * sqrt(lam));
+        out[d.woff[l] + k * wi + j] = e;
       }
     pi += (ard && l < h.L - 1) ? wi : 1;
   }
   for (int l = 0; l < h.L - 1; ++l) {
     const double lb = h.prec[pi + l];
-    const double cc = h.prior == BANN_STD_NORMAL ? 1.0 : c;
-    for (int k = 0; k < d.widths[l]; ++k) eps[d.boff[l] + k] = (float)(cc * PI / (2.0 * sqrt(lb) * lint));
+    const double e = PI / (2.0 * sqrt(lb));
+    for (int k = 0; k < d.widths[l]; ++k) out[d.boff[l] + k] = stdn ? -e : e;
   }
 }
 
@@ -305,10 +316,11 @@ static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
 
 static int ensure_htrace(bann_ctx* ctx, int32_t L) {
   if (L + 1 <= ctx->htrace_cap) return BANN_OK;
+  const int32_t cap = std::max({L + 1, 2 * ctx->htrace_cap, 129});  // grow geometrically: no realloc per trajectory
   dfree(ctx->d_htrace);
   ctx->d_htrace = nullptr;
-  CK(dalloc(&ctx->d_htrace, (int64_t)ctx->br.size() * (L + 1)));
-  ctx->htrace_cap = L + 1;
+  CK(dalloc(&ctx->d_htrace, (int64_t)ctx->br.size() * cap));
+  ctx->htrace_cap = cap;
   refresh_state(ctx);
   return BANN_OK;
 }
@@ -343,8 +355,10 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
-                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr};
+                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase};
   for (void* p : bufs) dfree(p);
+  if (ctx->h_status) (void)hipHostFree(ctx->h_status);
+  if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BANN_OK;
@@ -513,6 +527,8 @@ extern "C" int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b) {
   if (!check_branch(ctx, b)) return BANN_E_ARG;
   return ctx->br[b].dev.fused;
 }
+extern "C" const char* bann_fused_kernel_name(void) { return fused_kernel_family(); }
+
 extern "C" int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled) {
   if (!ctx) return BANN_E_ARG;
   if (ctx->finalized) return fail(ctx, BANN_E_STATE, "set before bann_finalize");
@@ -602,6 +618,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     CK(dalloc(pb, p_off));
     CK(hipMemsetAsync(*pb, 0, p_off * sizeof(float), ctx->stream));
   }
+  CK(dalloc(&ctx->d_stepbase, p_off));
   CK(dalloc(&ctx->d_part, part_off));
   CK(hipMemsetAsync(ctx->d_part, 0, part_off * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_rss_part, nb * max_splits));
@@ -611,6 +628,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_pred, nb * n));
   CK(hipMemsetAsync(ctx->d_pred, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_pred0, nb * n));
+  CK(dalloc(&ctx->d_delta, n));
+  CK(dalloc(&ctx->d_delta_part, residual_delta_scratch_floats(n)));
+  CK(hipHostMalloc((void**)&ctx->h_status, nb * sizeof(int32_t), hipHostMallocDefault));
+  CK(hipHostMalloc((void**)&ctx->h_delta, n * sizeof(float), hipHostMallocDefault));
   CK(hipMemsetAsync(ctx->d_pred0, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_scr, scr_off));
   CK(dalloc(&ctx->d_eprec, nb));
@@ -631,6 +652,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&d_idx, maxm));
   std::vector<BranchDev> descs;
   std::vector<float> lam, lamld, eprec(nb, 1.f);
+  std::vector<double> sbase;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
@@ -647,6 +669,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
                       ctx->stream));
     CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
                       ctx->stream));
+    step_bases(h, sbase);
+    CK(hipMemcpyAsync(ctx->d_stepbase + h.dev.p_off, sbase.data(), h.P * sizeof(double), hipMemcpyHostToDevice,
+                      ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));  // host vectors reused
   }
   dfree(d_idx);
   CK(dalloc(&ctx->d_br, nb));
@@ -696,6 +722,18 @@ extern "C" int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float*
   CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
                     ctx->stream));
   CK(hipMemcpyAsync(ctx->d_eprec + b, &ep, sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  std::vector<double> sbase;
+  step_bases(h, sbase);
+  CK(hipMemcpyAsync(ctx->d_stepbase + h.dev.p_off, sbase.data(), h.P * sizeof(double), hipMemcpyHostToDevice,
+                    ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_get_step_sizes(bann_ctx* ctx, int32_t b, float* out) {
+  if (!check_branch(ctx, b) || !out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  const BranchHost& h = ctx->br[b];
+  CK(hipMemcpyAsync(out, ctx->d_eps + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   return BANN_OK;
 }
@@ -742,6 +780,21 @@ extern "C" int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out) {
   if (rc) return rc;
   CK(hipMemcpyAsync(pred_out, ctx->d_pred + (int64_t)b * ctx->n, ctx->n * sizeof(float), hipMemcpyDeviceToHost,
                     ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_predict_many(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* pred_out) {
+  if (!ctx || !branches || nb <= 0 || !pred_out) return fail(ctx, BANN_E_ARG, "bad branch list or null output");
+  if (!ctx->finalized) return fail(ctx, BANN_E_STATE, "call bann_finalize first");
+  Plan p;
+  int rc = build_plan(ctx, branches, nb, p, false);
+  if (rc) return rc;
+  rc = run_grad(ctx, p, 1);  // one packed launch per kernel group, predictions written on the way
+  if (rc) return rc;
+  for (int32_t i = 0; i < nb; ++i)
+    CK(hipMemcpyAsync(pred_out + (int64_t)i * ctx->n, ctx->d_pred + (int64_t)branches[i] * ctx->n,
+                      ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   return BANN_OK;
 }
@@ -813,16 +866,24 @@ static int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, i
   std::mt19937_64 rng(seed ^ 0x5DEECE66Dull);
   std::vector<float> e;
   int64_t off = 0;
+  const bool device_eps = step_mode == BANN_STEP_UNIFORM || step_mode == BANN_STEP_IZMAILOV;
+  if (device_eps) {
+    launch_step_sizes(ctx->st, ctx->d_stepbase, p.d_all, (int32_t)p.all.size(), p.max_p,
+                      step_mode == BANN_STEP_UNIFORM ? 0 : 1, factor, L, ctx->stream);
+    CK(hipGetLastError());
+  }
   for (int32_t b : p.all) {
     const BranchHost& h = ctx->br[b];
-    if (step_mode == BANN_STEP_INJECTED) {
+    if (device_eps) {
+      // formed on the device above
+    } else if (step_mode == BANN_STEP_INJECTED) {
       if (!eps) return fail(ctx, BANN_E_ARG, "injected step sizes need eps");
       CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, eps + off, h.P * sizeof(float), hipMemcpyHostToDevice,
                         ctx->stream));
     } else {
-      if (step_mode != BANN_STEP_UNIFORM && step_mode != BANN_STEP_RANDOM && step_mode != BANN_STEP_IZMAILOV)
+      if (step_mode != BANN_STEP_RANDOM)
         return fail(ctx, BANN_E_ARG, "unsupported step size mode (StdScaled is not usable in the reference either)");
-      host_step_sizes(h, step_mode, factor, L, rng, e);
+      host_random_step_sizes(h, factor, rng, e);
       CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, e.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
                         ctx->stream));
     }
@@ -899,15 +960,18 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
                                    int32_t step_mode, float factor, uint64_t seed) {
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
   if (!branches || nb <= 0 || L < 1) return fail(ctx, BANN_E_ARG, "bad branch list or L");
-  int rc = build_plan(ctx, branches, nb, ctx->lf, true);
-  if (rc) return rc;
+  int rc = BANN_OK;
+  // the packed launch plan of a branch set is reused across trajectories (a sweep
+  // runs the same set every time); rebuild only when the set changes
+  if (!(ctx->lf.owns && ctx->lf.all.size() == (size_t)nb && std::equal(branches, branches + nb, ctx->lf.all.begin()))) {
+    rc = build_plan(ctx, branches, nb, ctx->lf, true);
+    if (rc) return rc;
+  }
   rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
   if (rc) return rc;
   rc = run_grad(ctx, ctx->lf, 1);
   if (rc) return rc;
-  for (int32_t b : ctx->lf.all)
-    CK(hipMemcpyAsync(ctx->d_pred0 + (int64_t)b * ctx->n, ctx->d_pred + (int64_t)b * ctx->n, ctx->n * sizeof(float),
-                      hipMemcpyDeviceToDevice, ctx->stream));
+  launch_snapshot_pred(ctx->st, ctx->lf.d_all, nb, ctx->stream);
   launch_update(ctx->st, ctx->lf.d_all, nb, MODE_INIT, 0, ctx->stream);
   CK(hipGetLastError());
   ctx->lf_active = true;
@@ -936,9 +1000,10 @@ extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* nu
     int rc = bann_leapfrog_steps(ctx, ctx->lf_L - ctx->lf_step);
     if (rc) return rc;
   }
+  CK(hipMemcpyAsync(ctx->h_status, ctx->d_status, ctx->br.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                    ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
-  std::vector<int32_t> st(ctx->br.size());
-  CK(hipMemcpy(st.data(), ctx->d_status, st.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  const int32_t* st = ctx->h_status;
   int acc = 0;
   for (size_t i = 0; i < ctx->lf.all.size(); ++i) {
     const int s = st[ctx->lf.all[i]];
@@ -953,9 +1018,22 @@ extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* nu
 extern "C" int bann_leapfrog_residual_delta_device(bann_ctx* ctx, float* out_device) {
   if (!ctx || !out_device) return BANN_E_ARG;
   if (ctx->lf.all.empty() || ctx->lf_active) return fail(ctx, BANN_E_STATE, "call after bann_leapfrog_end");
-  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), out_device, ctx->stream);
+  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->d_delta_part, out_device,
+                        ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_leapfrog_residual_delta(bann_ctx* ctx, float* out_host) {
+  if (!ctx || !out_host) return BANN_E_ARG;
+  if (ctx->lf.all.empty() || ctx->lf_active) return fail(ctx, BANN_E_STATE, "call after bann_leapfrog_end");
+  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->d_delta_part, ctx->d_delta,
+                        ctx->stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(ctx->h_delta, ctx->d_delta, ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  memcpy(out_host, ctx->h_delta, ctx->n * sizeof(float));
   return BANN_OK;
 }
 

@@ -112,4 +112,10 @@ void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int3
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
-void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s);
+const char* fused_kernel_family();  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
+void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
+                       int izmailov, float c, int32_t L, hipStream_t s);
+void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
+int64_t residual_delta_scratch_floats(int64_t n);
+void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* scratch, float* out,
+                           hipStream_t s);

@@ -854,19 +854,403 @@ __global__ void __launch_bounds__(64 * (NWMAX + 1))
   }
 }
 
-// BANN_FUSED_VARIANT: "reg" (default, register-staged lockstep kernel) or "pipe"
+// ---------------------------------------------------------------------------
+// MFMA-backward variant ("mx"): the pipelined schedule of k_fused_grad_pipe,
+// with dW0 = G^T delta0 ALSO on v_mfma_i32_16x16x64_i8 instead of VALU FMAs.
+//
+// The backward contracts over individuals, so its genotype operand is the
+// TRANSPOSE of the forward's (a lane needs 16 individuals of one marker, the
+// packed layout gives 16 markers of one individual).  The tile is already in
+// LDS (LDS-DMA ring), so the transpose is free: ds_read_b64_tr_b8 delivers,
+// per 16-lane group, column i of an 8-row x 16-byte block to lane i.
+//   * B (K = 64 individuals x N = 16 markers of sub-tile u): group g reads
+//     fragment g; read h covers individuals 8h .. 8h+7 of that fragment.
+//   * A (M = 4 columns x 4 digits, K = 64 individuals): the head wave writes
+//     delta0 of its individual as 16 signed digits (byte 4c + d) in a row of an
+//     [individual][16 B] image; the same transposed read yields A.
+// delta0 is quantised per tile and column with a power-of-two scale
+// s_c = 2^(E_c - 132) (E_c = the largest f32 exponent field in the column):
+// delta/s_c < 64, four digits of 7 bits carry 27 significant bits, so the
+// integer products are exact and the only roundings are the per-tile f32
+// accumulations (one per sub-tile and digit set).
+// The fragment stride in LDS is padded to 1152 B (and 384 B in the digit
+// image) so the two 16-lane groups of a half-wave read disjoint bank halves.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ float fpow2(uint32_t biased_exp) { return __builtin_bit_cast(float, biased_exp << 23); }
+
+typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t max_u16x2(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2u16, a), __builtin_bit_cast(v2u16, b)));
+}
+// wave-wide max of two packed u16 lanes (DPP row reductions, result uniform)
+__device__ __forceinline__ uint32_t wave_max_u16x2(uint32_t v) {
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast15
+  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+typedef int v2i __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) v2i lds_v2i;
+__device__ __forceinline__ v4i lds_tr8_pair(const char* p0, const char* p1) {
+  const v2i a = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0));
+  const v2i b = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p1));
+  return v4i{a.x, a.y, b.x, b.y};
+}
+
+// four signed 7-bit digits of v (|v| < 64), most significant first, packed LE
+__device__ __forceinline__ uint32_t digits4(float v) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const float r = __builtin_rintf(v);
+    w |= ((uint32_t)(int)r & 0xFFu) << (8 * d);
+    v = (v - r) * 128.f;
+  }
+  return w;
+}
+
+template <int NL, int NWMAX, int ACT>
+__global__ void __launch_bounds__(64 * (NWMAX + 1))
+    k_fused_grad_mx(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  constexpr int R = 3;
+  constexpr int NH = NL - 1;
+  constexpr int T = BANN_TILE_FRAGS;
+  static_assert(T == 4, "the backward MFMA contracts over exactly 4 fragments (64 individuals)");
+  constexpr int D = R - 2;       // prefetch distance in tiles
+  constexpr int SLAB = 1152;     // 1 KiB fragment slab + 128 B bank padding
+  constexpr int DROW = 384;      // digit image: 16 rows x 16 B + 128 B padding per fragment
+  __shared__ __attribute__((aligned(16))) char xr0[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) char xr1[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) char xr2[NWMAX * T * SLAB];
+  __shared__ __attribute__((aligned(16))) float yr0[64];
+  __shared__ __attribute__((aligned(16))) float yr1[64];
+  __shared__ __attribute__((aligned(16))) float yr2[64];
+  __shared__ __attribute__((aligned(16))) float s_zp[2][NWMAX][T][16][4];
+  __shared__ __attribute__((aligned(16))) char s_dig[2][T * DROW];
+  __shared__ __attribute__((aligned(16))) float s_scl[2][4];
+  __shared__ __attribute__((aligned(16))) HeadLds s_hd;
+  __shared__ __attribute__((aligned(16))) float s_db0[4];
+
+  const GradItem it = items[blockIdx.x];
+  const BranchDev& bd = st.br[it.branch];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = bd.nchunks;
+  const int64_t n = st.n;
+  const int fbeg = it.frag_begin, fend = it.frag_end, flast = fend - 1;
+  const int ntiles = (fend - fbeg + T - 1) / T;
+
+  for (int t = threadIdx.x; t < BANN_MAXL * 20; t += blockDim.x) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (l >= 1 && l < NL) {
+      if (r < 16) {
+        const int j = r >> 2, k = r & 3;
+        if (j < bd.win[l] && k < bd.widths[l]) v = st.theta[bd.p_off + bd.woff[l] + k * bd.win[l] + j];
+        s_hd.W[l][j][k] = v;
+      } else {
+        const int k = r - 16;
+        if (l < NL - 1 && k < bd.widths[l]) v = st.theta[bd.p_off + bd.boff[l] + k];
+        s_hd.bias[l][k] = v;
+      }
+    } else if (l == 0 && r >= 16) {
+      const int k = r - 16;
+      s_hd.bias[0][k] = (k < bd.widths[0]) ? st.fc[it.branch].c0[k] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+
+  if (wave == 0) {
+    // ===================== head wave =====================
+    const int64_t y_off = bd.y_off;
+    const float* ybr = st.y + y_off;
+    float* predb = st.pred + y_off;
+    auto yslot = [&](auto sc) -> float* {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) return yr0;
+      else if constexpr (s == 1) return yr1;
+      else return yr2;
+    };
+    auto issue_y = [&](int t, auto sc) {
+      const int64_t row = (int64_t)min(fbeg + t * T + (lane >> 4), flast) * 16 + (lane & 15);
+      glds4(ybr + (row < n ? row : n - 1), yslot(sc));
+    };
+    double rss = 0.0;
+    float db[NH][4], dWo[4];
+    float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dWo[k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+    }
+    issue_y(0, std::integral_constant<int, 0>{});
+    auto head_iter = [&](int t, auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (t < ntiles) issue_y(t + D, std::integral_constant<int, (s + D) % R>{});
+      LDS_BARRIER();
+      if (t == ntiles) return;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");  // y(t) landed (y(t+D) may fly)
+      const int q = lane >> 4, rr = lane & 15;
+      const int f = fbeg + t * T + q;
+      const int64_t row = (int64_t)f * 16 + rr;
+      const bool valid = (f < fend) && (row < n);
+      const float yv = yslot(sc)[lane];
+      const int zb = t & 1;
+      float d[4];
+#if BANN_ABLATE & 1
+      {
+        const v4f p0 = *reinterpret_cast<const v4f*>(&s_zp[zb][0][q][rr][0]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = valid ? p0[k] * 1e-3f - yv : 0.f;
+      }
+#else
+      float z[NH][4], a[NH][4];
+      v4f zs = *reinterpret_cast<const v4f*>(&s_hd.bias[0][0]);
+#pragma unroll
+      for (int w = 0; w < NWMAX; ++w) {
+        const v4f p = *reinterpret_cast<const v4f*>(&s_zp[zb][w][q][rr][0]);  // chunk-less waves wrote 0
+        zs += p;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[0][k] = zs[k];
+        a[0][k] = act_h_t<ACT>(z[0][k]);
+      }
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float sacc = s_hd.bias[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc = fmaf(a[l - 1][j], s_hd.W[l][j][k], sacc);
+          z[l][k] = sacc;
+          a[l][k] = act_h_t<ACT>(sacc);
+        }
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], s_hd.W[NL - 1][j][0], out);
+      const float e = valid ? out - yv : 0.f;
+      if (write_pred && valid) predb[row] = out;
+      rss += (double)e * (double)e;
+      float err[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+        err[j] = e * s_hd.W[NL - 1][j][0];
+      }
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        float dl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dl[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
+          db[l][k] += dl[k];
+        }
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float sj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dW[l - 1][j][k] = fmaf(a[l - 1][j], dl[k], dW[l - 1][j][k]);
+              sj = fmaf(dl[k], s_hd.W[l][j][k], sj);
+            }
+            err[j] = sj;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = dl[k];
+        }
+      }
+#endif
+      // ---- delta0 -> per-column power-of-two scale + 4 digits (A image) ----
+      const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+      const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+      const uint32_t E[4] = {e01 & 0xFFFFu, e01 >> 16, e23 & 0xFFFFu, e23 >> 16};
+      v4i w;
+      v4f scl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = E[k] >= 6u;   // columns below 2^-121 (or all zero) contribute 0
+        const float inv = ok ? fpow2(259u - E[k]) : 0.f;
+        scl[k] = ok ? fpow2(E[k] - 5u) : 0.f;
+        w[k] = (int)digits4(d[k] * inv);
+      }
+      asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(&s_dig[zb][q * DROW + rr * 16])), "v"(w) : "memory");
+      if (lane == 0) lds_st_v4f(reinterpret_cast<v4f*>(&s_scl[zb][0]), scl);
+    };
+    for (int t = 0; t <= ntiles; t += 3) {
+      head_iter(t, std::integral_constant<int, 0>{});
+      if (t + 1 > ntiles) break;
+      head_iter(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 > ntiles) break;
+      head_iter(t + 2, std::integral_constant<int, 2>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double rs = wave_sum_d(rss);
+    float db0s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db0s[k] = wave_sum(db[0][k]);
+    if (lane == 0) {
+      st.rss_part[(int64_t)it.branch * st.max_splits + it.split] = rs;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s_db0[k] = db0s[k];
+        if (k < bd.widths[0]) part[bd.boff[0] + k] = db0s[k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = wave_sum(dWo[j]);
+      if (lane == 0 && j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = wave_sum(db[l][k]);
+        if (lane == 0 && k < bd.widths[l]) part[bd.boff[l] + k] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float wv = wave_sum(dW[l - 1][j][k]);
+          if (lane == 0 && j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = wv;
+        }
+      }
+    }
+    __syncthreads();  // s_db0 visible to the chunk waves
+  } else {
+    // ===================== chunk waves =====================
+    const int cw = wave - 1;
+    const bool has_chunk = cw < nch;
+    const int mych = has_chunk ? cw : nch - 1;
+    float scale = has_chunk ? st.fc[it.branch].scale[lane >> 4] : 0.f;  // chunk-less: zp = 0
+    v4i adig = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)mych * 64 + lane) * 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(adig), "+v"(scale));
+    const int64_t frag_bytes = (int64_t)nch * 1024;
+    const int8_t* xw = st.xpk + bd.x_off + ((int64_t)mych * 64 + lane) * 16;
+    auto xslot = [&](auto sc) -> char* {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) return xr0 + cw * T * SLAB;
+      else if constexpr (s == 1) return xr1 + cw * T * SLAB;
+      else return xr2 + cw * T * SLAB;
+    };
+    auto issue_x = [&](int t, auto sc) {
+      char* base = xslot(sc);
+#pragma unroll
+      for (int q = 0; q < T; ++q) {
+        const int f = min(fbeg + t * T + q, flast);
+        glds16(xw + (int64_t)f * frag_bytes, base + q * SLAB);
+      }
+    };
+    // transposed-read address of this lane inside a fragment-padded image:
+    // group g = lane >> 4 -> fragment g; lane 2r + p -> row r, bytes 8p .. 8p+7
+    const int tr_off = (lane & 15) / 2 * 16 + 8 * (lane & 1);
+    float dw[4] = {0.f, 0.f, 0.f, 0.f};  // dW0 (G^T delta0) of column lane>>4, marker 16u + (lane & 15)
+    issue_x(0, std::integral_constant<int, 0>{});
+    auto chunk_iter = [&](int t, auto sc) {
+      constexpr int s = decltype(sc)::value;
+      if (t < ntiles) {
+        issue_x(t + D, std::integral_constant<int, (s + D) % R>{});  // clamped: always valid
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T * D) : "memory");  // X(t) landed, X(t+D) in flight
+        const char* xs = xslot(sc) + lane * 16;
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          const v4i xv = *reinterpret_cast<const v4i*>(xs + q * SLAB);
+#if BANN_ABLATE & 4
+          v4i d = xv;
+#else
+          v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig, xv, v4i{0, 0, 0, 0}, 0, 0, 0);
+#endif
+          const float zp = scale * ((float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f +
+                                    (float)d[3] * 0x1p-21f);
+          lds_st_f32(&s_zp[t & 1][cw][q][lane & 15][lane >> 4], zp);
+        }
+      }
+      LDS_BARRIER();
+      if (t >= 1 && has_chunk) {
+        const int tb = t - 1;
+        const char* xs = xslot(std::integral_constant<int, (s + R - 1) % R>{}) + (lane >> 4) * SLAB + tr_off;
+        const char* ds = &s_dig[tb & 1][0] + (lane >> 4) * DROW + tr_off;
+        const v4i A = lds_tr8_pair(ds, ds + 8 * 16);
+        const float sc_c = s_scl[tb & 1][lane >> 4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const v4i B = lds_tr8_pair(xs + u * 256, xs + u * 256 + 8 * 16);
+#if BANN_ABLATE & 2
+          asm volatile("" ::"v"(A), "v"(B));
+#else
+          const v4i g = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, v4i{0, 0, 0, 0}, 0, 0, 0);
+          const float v = (float)g[0] + (float)g[1] * 0x1p-7f + (float)g[2] * 0x1p-14f + (float)g[3] * 0x1p-21f;
+          dw[u] = fmaf(sc_c, v, dw[u]);
+#endif
+        }
+      }
+    };
+    for (int t = 0; t <= ntiles; t += 3) {
+      chunk_iter(t, std::integral_constant<int, 0>{});
+      if (t + 1 > ntiles) break;
+      chunk_iter(t + 1, std::integral_constant<int, 1>{});
+      if (t + 2 > ntiles) break;
+      chunk_iter(t + 2, std::integral_constant<int, 2>{});
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // s_db0 published by the head wave
+    if (has_chunk) {
+      const int c = lane >> 4;
+      if (c < bd.widths[0]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int sidx = cw * 64 + u * 16 + (lane & 15);
+          if (sidx < bd.m) {
+            const float mu = st.mu[bd.mk_off + sidx], sg = st.sigma[bd.mk_off + sidx];
+            part[bd.woff[0] + c * bd.m + sidx] = sg > 0.f ? (dw[u] - mu * s_db0[c]) / sg : 0.f;
+          }
+        }
+      }
+    }
+  }
+}
+
+// BANN_FUSED_VARIANT: "mx" (default: MFMA backward), "pipe" (VALU backward,
+// dedicated head wave) or "reg" (register-staged lockstep kernel)
 static int fused_variant() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("BANN_FUSED_VARIANT");
-    v = (e && e[0] == 'p') ? 2 : 0;
+    v = (e && e[0] == 'p') ? 2 : (e && e[0] == 'r') ? 0 : 3;
   }
   return v;
+}
+
+const char* fused_kernel_family() {
+  switch (fused_variant()) {
+    case 3: return "k_fused_grad_mx";
+    case 2: return "k_fused_grad_pipe";
+    default: return "k_fused_grad";
+  }
 }
 
 template <int NL, int ACT>
 static void launch_fused_t(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int wp,
                            hipStream_t s) {
+  if (fused_variant() == 3 && nwaves <= 8) {
+    hipLaunchKernelGGL((k_fused_grad_mx<NL, 8, ACT>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
+    return;
+  }
   if (fused_variant() == 2 && nwaves <= 8) {  // > 8 chunks: the LDS ring would not fit; use the reg kernel
     hipLaunchKernelGGL((k_fused_grad_pipe<NL, 8, ACT, 3>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
     return;

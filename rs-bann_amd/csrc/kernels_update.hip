@@ -255,19 +255,99 @@ void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t
 
 // residual change of a finished trajectory (net.rs:292-300): accepted branches
 // replace their previous prediction by f(theta_L); rejected ones leave it.
-__global__ void k_residual_delta(DevState st, const int32_t* __restrict__ blist, int nb, float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= st.n) return;
-  float acc = 0.f;
-  for (int q = 0; q < nb; ++q) {
+// Two passes, deterministic: RD_GROUPS branch slices each sum their accepted
+// branches into a partial row (4 individuals per thread, the q loop unrolled so
+// several pred/pred0 loads are in flight), then the rows are added in order.
+constexpr int RD_GROUPS = 16;
+__global__ void __launch_bounds__(256) k_residual_delta_part(DevState st, const int32_t* __restrict__ blist, int nb,
+                                                             float* __restrict__ part) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= st.n) return;
+  const int g = blockIdx.y;
+  const int q0 = (int)((int64_t)nb * g / RD_GROUPS), q1 = (int)((int64_t)nb * (g + 1) / RD_GROUPS);
+  const bool full = i0 + 4 <= st.n && (st.n & 3) == 0;  // float4 path needs 16-byte aligned rows
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+  for (int q = q0; q < q1; ++q) {
     const int b = blist[q];
     if (st.status[b] != ST_ACCEPTED) continue;
-    const int64_t o = (int64_t)b * st.n + i;
-    acc += st.pred[o] - st.pred0[o];
+    const int64_t o = (int64_t)b * st.n + i0;
+    if (full) {
+      const float4 p = *reinterpret_cast<const float4*>(st.pred + o);
+      const float4 r = *reinterpret_cast<const float4*>(st.pred0 + o);
+      a0 += p.x - r.x;
+      a1 += p.y - r.y;
+      a2 += p.z - r.z;
+      a3 += p.w - r.w;
+    } else {
+      a0 += st.pred[o] - st.pred0[o];
+      if (i0 + 1 < st.n) a1 += st.pred[o + 1] - st.pred0[o + 1];
+      if (i0 + 2 < st.n) a2 += st.pred[o + 2] - st.pred0[o + 2];
+      if (i0 + 3 < st.n) a3 += st.pred[o + 3] - st.pred0[o + 3];
+    }
   }
+  float* row = part + (int64_t)g * st.n + i0;
+  row[0] = a0;
+  if (i0 + 1 < st.n) row[1] = a1;
+  if (i0 + 2 < st.n) row[2] = a2;
+  if (i0 + 3 < st.n) row[3] = a3;
+}
+
+__global__ void k_residual_delta_sum(const float* __restrict__ part, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float acc = 0.f;
+#pragma unroll
+  for (int g = 0; g < RD_GROUPS; ++g) acc += part[(int64_t)g * n + i];
   out[i] = acc;
 }
 
-void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_residual_delta, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, st, branches, nb, out);
+int64_t residual_delta_scratch_floats(int64_t n) { return (int64_t)RD_GROUPS * n; }
+
+void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* scratch, float* out,
+                           hipStream_t s) {
+  const unsigned gx = (unsigned)((st.n + 1023) / 1024);
+  hipLaunchKernelGGL(k_residual_delta_part, dim3(gx, RD_GROUPS), dim3(256), 0, s, st, branches, nb, scratch);
+  hipLaunchKernelGGL(k_residual_delta_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, scratch, st.n, out);
+}
+
+// pred0 <- pred for the listed branches (trajectory start), one launch
+__global__ void __launch_bounds__(256) k_snapshot_pred(DevState st, const int32_t* __restrict__ blist) {
+  const int b = blist[blockIdx.y];
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t o = (int64_t)b * st.n + i;
+  if (i + 4 <= st.n && (st.n & 3) == 0) {
+    *reinterpret_cast<float4*>(st.pred0 + o) = *reinterpret_cast<const float4*>(st.pred + o);
+  } else {
+    for (int k = 0; k < 4 && i + k < st.n; ++k) st.pred0[o + k] = st.pred[o + k];
+  }
+}
+
+void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_snapshot_pred, dim3((unsigned)((st.n + 1023) / 1024), (unsigned)nb), dim3(256), 0, s, st,
+                     branches);
+}
+
+// step sizes on the device (uniform 706-732; izmailov: see step_bases in
+// bann_api.hip): eps = c, or |base| * (base > 0 ? c : 1) / L, rounded once to f32
+__global__ void __launch_bounds__(256) k_step_sizes(DevState st, const double* __restrict__ base,
+                                                    const int32_t* __restrict__ blist, int izmailov, float c, int L) {
+  const int b = blist[blockIdx.y];
+  const BranchDev bd = st.br[b];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= bd.P) return;
+  float e = c;
+  if (izmailov) {
+    const double v = base[bd.p_off + i];
+    e = (float)(v > 0.0 ? (double)c * v / (double)L : -v / (double)L);
+  }
+  st.eps[bd.p_off + i] = e;
+}
+
+void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
+                       int izmailov, float c, int32_t L, hipStream_t s) {
+  if (nb <= 0 || max_p <= 0) return;
+  hipLaunchKernelGGL(k_step_sizes, dim3((unsigned)((max_p + 255) / 256), (unsigned)nb), dim3(256), 0, s, st, base,
+                     branches, izmailov, c, L);
 }

@@ -154,6 +154,21 @@ def test_multi_branch_packed(Ctx):
     ctx.close()
 
 
+def test_predict_many_matches_predict(Ctx):
+    rng = np.random.default_rng(17)
+    n, m, nb = 901, 96, 6
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = [dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, [4, 4, 1] if b % 2 else [3, 1])),
+                  y=rng.normal(size=n)) for b in range(nb)]
+    ctx = build_context(Ctx, g, specs)
+    order = [4, 0, 5, 2]
+    many = ctx.predict_many(order)
+    for i, b in enumerate(order):
+        assert np.array_equal(many[i], ctx.predict(b))
+    ctx.close()
+
+
 def test_gradient_deterministic_and_split_invariant(Ctx):
     rng, g, snps, br = make_problem(dict(n=4000, m=500, widths=[4, 4, 1], act="tanh", prior="ridge_ard"), 3)
     y = rng.normal(size=4000)
@@ -247,6 +262,31 @@ def test_hmc_packed_equals_individual(Ctx):
         ctx.close()
 
 
+@pytest.mark.parametrize("mode", ["izmailov", "uniform"])
+def test_device_step_sizes_match_oracle(Ctx, mode):
+    """Izmailov / uniform step sizes formed on the device equal the oracle's
+    (izmailov_step_sizes of the five priors, branch_sampler.rs:706-732)."""
+    rng = np.random.default_rng(31)
+    n, m = 128, 40
+    priors = ["ridge_ard", "ridge_base", "lasso_ard", "lasso_base", "std_normal"]
+    g = O.synthetic_genotypes(rng, n, m * len(priors))
+    specs = [dict(snps=np.arange(k * m, (k + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, [4, 3, 1], prior=p)), y=rng.normal(size=n))
+             for k, p in enumerate(priors)]
+    ctx = build_context(Ctx, g, specs)
+    L, c = 7, 0.37
+    ctx.leapfrog_begin(list(range(len(priors))), L, 10.0, mode, c, seed=1)
+    ctx.leapfrog_end()
+    for k, s in enumerate(specs):
+        got = ctx.get_step_sizes(k)
+        if mode == "uniform":
+            ref = np.full(got.size, np.float32(c))
+        else:
+            ref = O.param_vec(*O.izmailov_step_sizes(s["branch"], c, L)).astype(np.float32)
+        assert np.allclose(got, ref, rtol=2e-7, atol=0), (priors[k], np.max(np.abs(got / ref - 1)))
+    ctx.close()
+
+
 def test_leapfrog_session_matches_hmc_step(Ctx):
     """The benchmark entry points (begin/steps/end, device RNG) run the same
     integrator: with L steps they leave every branch accepted/rejected with
@@ -271,6 +311,42 @@ def test_leapfrog_session_matches_hmc_step(Ctx):
         assert np.all(np.isfinite(after))
         if status[b] != 0:
             assert np.array_equal(after, before[b])
+    ctx.close()
+
+
+@pytest.mark.parametrize("n", [1003, 2048])
+def test_residual_delta_matches_oracle(Ctx, n):
+    """residual change of a trajectory (net.rs:279-300 bookkeeping): the sum over
+    accepted branches of f_b(theta_L) - f_b(theta_0), from both the host and the
+    device entry points, against the oracle predictions of the same params."""
+    rng = np.random.default_rng(5 + n)
+    nb, m = 37, 64
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = []
+    for b in range(nb):
+        br = f32_branch(O.random_branch(rng, m, [4, 4, 1]))
+        specs.append(dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32), branch=br, y=rng.normal(size=n)))
+    ctx = build_context(Ctx, g, specs)
+    mu, sd = ctx.genotype_stats()
+    before = [ctx.get_params(b) for b in range(nb)]
+    ctx.leapfrog_begin(list(range(nb)), 6, 1.0, "izmailov", 0.5, seed=9)
+    ctx.leapfrog_steps(6)
+    status, acc = ctx.leapfrog_end()
+    assert acc > 0
+    got = ctx.residual_delta().astype(np.float64)
+    ref = np.zeros(n)
+    for b in range(nb):
+        if status[b] != 0:
+            continue
+        X = x_std(g[b * m:(b + 1) * m], mu[b * m:(b + 1) * m], sd[b * m:(b + 1) * m])
+        br = specs[b]["branch"]
+        w1, b1 = layer_views(br, ctx.get_params(b))
+        w0, b0 = layer_views(br, before[b])
+        new, old = br.copy(), br.copy()
+        new.weights, new.biases = w1, b1
+        old.weights, old.biases = w0, b0
+        ref += O.predict(new, X) - O.predict(old, X)
+    assert np.max(np.abs(got - ref)) <= 1e-4 * max(1.0, np.max(np.abs(ref)))
     ctx.close()
 
 

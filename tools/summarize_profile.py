@@ -1,0 +1,76 @@
+"""Condense a tools/profile_round.sh run into committed files under profiles/:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary of the bench command
+  profiles/<tag>_summary.md         per-kernel table (timed-trajectory launches) + PMC traffic
+  profiles/<tag>_pmc.json           HBM bytes per gradient launch (gfx950-corrected)
+usage: python tools/summarize_profile.py <tag> <out_dir>"""
+import csv, glob, json, os, shutil, statistics, sys
+
+tag, out = sys.argv[1], sys.argv[2]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(root, "profiles")
+os.makedirs(prof, exist_ok=True)
+
+
+def find(sub, pattern):
+    hits = glob.glob(os.path.join(out, sub, "**", pattern), recursive=True)
+    return hits[0] if hits else None
+
+
+stats = find("trace", "*kernel_stats.csv")
+shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+trace = list(csv.DictReader(open(find("trace", "*kernel_trace.csv"))))
+bench = json.loads(open(os.path.join(out, "bench_trace.json")).read().strip().splitlines()[-1])
+
+# launches of the gradient kernel over the full branch set (grid = items x 576 threads)
+grad = [r for r in trace if "k_fused_grad" in r["Kernel_Name"]]
+big = max(int(r["Grid_Size_X"]) for r in grad)
+full = [r for r in grad if int(r["Grid_Size_X"]) == big]
+dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in full]
+upd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace
+       if "k_update" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == max(
+           int(x["Grid_Size_X"]) for x in trace if "k_update" in x["Kernel_Name"])]
+
+
+def pmc_bytes(sub, counter):
+    f = find(sub, "*counter_collection.csv")
+    rows = list(csv.DictReader(open(f)))
+    per = {}
+    for r in rows:
+        if "k_fused_grad" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            per.setdefault(key, [int(r["Grid_Size"]) if "Grid_Size" in r else 0, 0.0])
+            per[key][1] += float(r["Counter_Value"])
+    vals = [v for g, v in per.values()]
+    gmax = max(g for g, v in per.values())
+    vals = [v for g, v in per.values() if g == gmax]
+    return statistics.median(vals) * 1024.0  # rocprofv3 reports KB
+
+
+fetch = pmc_bytes("fetch", "FETCH_SIZE") * 2.0   # gfx950: FETCH_SIZE counts 1/2 of wide streaming reads
+write = pmc_bytes("write", "WRITE_SIZE")
+pmc = {"kernel": full[0]["Kernel_Name"], "config": bench["config"]["workload"],
+       "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+       "traffic_bytes_per_launch": fetch + write,
+       "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+       "note": "FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md HBM), WRITE_SIZE as reported; "
+               "median over the full-branch-set launches of a separate --pmc pass"}
+json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
+
+with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
+    f.write(f"# Profile {tag}: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline`\n\n")
+    f.write(f"workload: {bench['config']['workload']}\n\n")
+    f.write(f"bench line under the profiler: value {bench['value']:.2f} {bench['unit']}, "
+            f"ms_per_step {bench['ms_per_step']:.3f}\n\n")
+    f.write("| kernel | launches (full branch set) | mean ms | median ms | min ms |\n|---|---|---|---|---|\n")
+    f.write(f"| {full[0]['Kernel_Name']} | {len(dur)} | {statistics.mean(dur):.3f} | "
+            f"{statistics.median(dur):.3f} | {min(dur):.3f} |\n")
+    f.write(f"| k_update (full set) | {len(upd)} | {statistics.mean(upd):.3f} | {statistics.median(upd):.3f} | "
+            f"{min(upd):.3f} |\n\n")
+    f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.3f} ms\n\n")
+    f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB; "
+            f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
+    f.write(f"achieved (algorithmic bytes / median launch): "
+            f"{pmc['alg_bytes_per_launch'] / (statistics.median(dur) * 1e-3) / 1e9:.0f} GB/s\n\n")
+    f.write("Full per-kernel stats of the command (all launches, setup included): "
+            f"`{tag}_kernel_stats.csv`.\n")
+print(open(os.path.join(prof, f"{tag}_summary.md")).read())
