@@ -84,10 +84,10 @@ def cpu_baseline(n, m, widths, sample_branches, sample_steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)   # L = 100: the reference default integration length (mcmc_cfg.rs:38)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--step-factor", type=float, default=0.5)
+    ap.add_argument("--step-factor", type=float, default=1.0)   # cli.rs:99-100 default
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-branches", type=int, default=96)
     ap.add_argument("--cpu-sample-steps", type=int, default=16)
@@ -106,10 +106,11 @@ def main():
         dist = dist_mod
 
     from bann import BannContext
+    from bann.distributed import allreduce_sum_, shard_ranges
 
     n, M_total, B_total, widths = CONFIGS[args.config]
     m_b = M_total // B_total
-    b0, b1 = rank * B_total // world, (rank + 1) * B_total // world
+    b0, b1 = shard_ranges([m_b] * B_total, world)[rank]   # contiguous, balanced by markers
     nb = b1 - b0
 
     t_setup = time.time()
@@ -172,7 +173,7 @@ def main():
         status, acc = ctx.leapfrog_end()
         if dist is not None:
             ctx.residual_delta_device(delta.data_ptr())
-            dist.all_reduce(delta)
+            allreduce_sum_(delta, dist)       # RCCL over xGMI: the sweep-level residual exchange
             torch.cuda.synchronize()
         else:   # one GPU: no torch in the process (rocprofv3 + torch's HIP runtime do not mix here)
             ctx.residual_delta()
