@@ -98,11 +98,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = os.environ.get("BANN_DIST_BACKEND", "nccl")   # gloo: rehearse N ranks on one GPU
+    dist_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist_mod
+        local_rank = local_rank % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local_rank)
-        dist_mod.init_process_group("nccl", init_method="env://")
+        dist_mod.init_process_group(backend, init_method="env://")
         dist = dist_mod
 
     from bann import BannContext
@@ -131,7 +134,7 @@ def main():
     tot = np.array([out_ss, float(nb)])
     if dist is not None:
         import torch
-        tt = torch.tensor(tot, device="cuda")
+        tt = torch.tensor(tot, device=dist_dev)
         dist.all_reduce(tt)
         tot = tt.cpu().numpy()
     out_prec = tot[1] / tot[0]
@@ -145,7 +148,7 @@ def main():
     fsum += preds.sum(axis=0, dtype=np.float64)
     if dist is not None:
         import torch
-        tt = torch.tensor(fsum, device="cuda")
+        tt = torch.tensor(fsum, device=dist_dev)
         dist.all_reduce(tt)
         fsum = tt.cpu().numpy()
     # phenotype y = sum_b f_b + noise at h^2 = 0.5; residual = noise; each branch
@@ -173,7 +176,12 @@ def main():
         status, acc = ctx.leapfrog_end()
         if dist is not None:
             ctx.residual_delta_device(delta.data_ptr())
-            allreduce_sum_(delta, dist)       # RCCL over xGMI: the sweep-level residual exchange
+            if backend == "nccl":
+                allreduce_sum_(delta, dist)   # RCCL over xGMI: the sweep-level residual exchange
+            else:
+                dc = delta.cpu()
+                allreduce_sum_(dc, dist)
+                delta.copy_(dc)
             torch.cuda.synchronize()
         else:   # one GPU: no torch in the process (rocprofv3 + torch's HIP runtime do not mix here)
             ctx.residual_delta()
@@ -193,10 +201,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        te = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        te = torch.tensor([elapsed], device=dist_dev, dtype=torch.float64)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         elapsed = float(te.item())
-        ta = torch.tensor([acc, nb], device="cuda", dtype=torch.float64)
+        ta = torch.tensor([acc, nb], device=dist_dev, dtype=torch.float64)
         dist.all_reduce(ta)
         acc_all, nb_all = float(ta[0]), float(ta[1])
     else:
@@ -221,7 +229,7 @@ def main():
     traffic, traffic_src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         pm = json.load(open(f))
-        if pm.get("config") == workload and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
+        if world == 1 and pm.get("config") == workload and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
             traffic, traffic_src = pm["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
             break
 

@@ -62,6 +62,8 @@ struct bann_ctx {
   // device buffers
   BranchDev* d_br = nullptr;
   int8_t* d_xpk = nullptr;
+  uint8_t* d_xu2 = nullptr;  // 2-bit packed genotypes of the fused branches (u2 format)
+  bool u2 = false;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;
@@ -130,6 +132,8 @@ static void refresh_state(bann_ctx* ctx) {
   DevState& s = ctx->st;
   s.br = ctx->d_br;
   s.xpk = ctx->d_xpk;
+  s.xu2 = ctx->d_xu2;
+  s.u2 = ctx->u2 ? 1 : 0;
   s.dig = ctx->d_dig;
   s.fc = ctx->d_fc;
   s.mu = ctx->d_mub;
@@ -255,15 +259,15 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       p.max_p_generic = std::max(p.max_p_generic, h.P);
       continue;
     }
-    const int grp = (h.L - 2) * 5 + h.act;
-    const int64_t nfrag = ctx->nfrag;
+    const int grp = ((h.L - 2) * 5 + h.act) * 2 + (h.dev.nchunks > 8 ? 1 : 0);
+    const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
     const int ns = h.dev.nsplits;
-    for (int s = 0; s < ns; ++s) {
+    for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
       GradItem it;
       it.branch = b;
       it.split = s;
-      it.frag_begin = (int32_t)(nfrag * s / ns);
-      it.frag_end = (int32_t)(nfrag * (s + 1) / ns);
+      it.frag_begin = (int32_t)(BANN_TILE_FRAGS * (ntile * s / ns));
+      it.frag_end = (int32_t)std::min<int64_t>(nfrag, BANN_TILE_FRAGS * (ntile * (s + 1) / ns));
       p.items[grp].push_back(it);
     }
     p.nwaves[grp] = std::max(p.nwaves[grp], h.dev.nchunks);
@@ -306,7 +310,7 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
   for (int g = 0; g < BANN_NGROUPS; ++g)
     if (!p.items[g].empty())
-      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 5 + 2, g % 5,
+      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 10 + 2, (g / 2) % 5,
                         write_pred, ctx->stream);
   if (!p.generic.empty())
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
@@ -351,7 +355,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   free_plan(ctx->lf);
-  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_dig, ctx->d_fc, ctx->d_mub,
+  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_xu2, ctx->d_dig, ctx->d_fc, ctx->d_mub,
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
@@ -564,13 +568,34 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   if (const char* e = getenv("BANN_MIN_FRAGS")) min_frags = std::max<int64_t>(1, atoll(e));
   const int64_t frags_per_item =
       std::max<int64_t>(min_frags, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
-  int64_t x_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
+  // genotype storage of the fused branches: 2-bit codes when the kernel family
+  // reads them and every genotype is a 2-bit value (0..3), else int8
+  ctx->u2 = false;
+  if (fused_prefers_u2() && total_frags > 0) {
+    int32_t* d_flag = nullptr;
+    int32_t flag = 0;
+    CK(dalloc(&d_flag, 1));
+    CK(hipMemsetAsync(d_flag, 0, sizeof(int32_t), ctx->stream));
+    launch_check_2bit(ctx->d_g, n * ctx->M, d_flag, ctx->stream);
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(&flag, d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    dfree(d_flag);
+    ctx->u2 = flag == 0;
+  }
+  const int64_t ntile = (ctx->nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
+  int64_t x_off = 0, x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     BranchDev& d = h.dev;
-    d.x_off = x_off;
-    x_off += (int64_t)ctx->nfrag * d.nchunks * 1024;
+    if (d.fused && ctx->u2 && d.nchunks <= 8) {  // the register-staged kernel serves <= 8 chunks
+      d.x_off = x2_off;  // byte offset into the 2-bit buffer: [tile][chunk][64 lanes][16 B]
+      x2_off += ntile * d.nchunks * 1024;
+    } else {
+      d.x_off = x_off;
+      x_off += (int64_t)ctx->nfrag * d.nchunks * 1024;
+    }
     d.dig_off = dig_off;
     if (d.fused) dig_off += (int64_t)d.nchunks * 1024;
     d.p_off = p_off;
@@ -579,7 +604,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     mk_off += h.m;
     d.y_off = (int64_t)b * n;
     d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
-    d.nsplits = std::min<int32_t>(d.nsplits, ctx->nfrag);
+    d.nsplits = (int32_t)std::min<int64_t>(d.nsplits, ntile);
     max_splits = std::max(max_splits, d.nsplits);
     d.part_off = part_off;
     part_off += (int64_t)d.nsplits * h.P;
@@ -602,10 +627,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     }
   }
   ctx->max_splits = max_splits;
-  ctx->packed_bytes = x_off;
+  ctx->packed_bytes = x_off + x2_off;
   ctx->total_p = p_off;
   const int64_t nb = (int64_t)ctx->br.size();
-  CK(dalloc(&ctx->d_xpk, x_off));
+  CK(dalloc(&ctx->d_xpk, std::max<int64_t>(x_off, 16)));
+  if (x2_off) CK(dalloc(&ctx->d_xu2, x2_off));
   CK(dalloc(&ctx->d_dig, dig_off));
   CK(hipMemsetAsync(ctx->d_dig, 0, (size_t)std::max<int64_t>(dig_off, 1), ctx->stream));
   CK(dalloc(&ctx->d_fc, nb));
@@ -656,7 +682,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    launch_pack_branch(ctx->d_g, d_idx, h.m, n, ctx->d_xpk + h.dev.x_off, h.dev.nchunks, ctx->nfrag, ctx->stream);
+    if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8)
+      launch_pack_branch_u2(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
+                            ctx->stream);
+    else
+      launch_pack_branch(ctx->d_g, d_idx, h.m, n, ctx->d_xpk + h.dev.x_off, h.dev.nchunks, ctx->nfrag, ctx->stream);
     launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, h.m, ctx->d_mub + h.dev.mk_off, ctx->d_sigb + h.dev.mk_off,
                         ctx->stream);
     CK(hipGetLastError());

@@ -57,7 +57,8 @@ struct FusedConst {
 
 struct DevState {
   const BranchDev* br;    // [nbranch]
-  const int8_t* xpk;      // packed genotypes
+  const int8_t* xpk;      // packed int8 genotypes ([frag][chunk][lane][16 B])
+  const uint8_t* xu2;     // packed 2-bit genotypes ([tile][chunk][lane][4 x u32]), fused branches
   const uint8_t* dig;     // digits
   FusedConst* fc;         // [nbranch]
   const float* mu;        // gathered per-branch marker means  [sum m]
@@ -88,6 +89,7 @@ struct DevState {
   int32_t max_splits;
   int32_t lint;           // trajectory length L (for the trace stride)
   float max_dh;
+  int32_t u2;             // fused branches read xu2 (2-bit) instead of xpk
 };
 
 // ---- launchers (defined in the kernel translation units) ----
@@ -104,7 +106,7 @@ void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp
 
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
                        int32_t act, int write_pred, hipStream_t s);
-#define BANN_NGROUPS 15  // fused launch groups: (L - 2) * 5 + activation, L in [2, 4]
+#define BANN_NGROUPS 30  // fused launch groups: ((L - 2) * 5 + activation) * 2 + (nchunks > 8), L in [2, 4]
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
@@ -112,7 +114,11 @@ void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int3
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
-const char* fused_kernel_family();  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
+const char* fused_kernel_family();
+int fused_prefers_u2();             // the fused variant reads 2-bit genotypes unless BANN_GENO_FORMAT=i8
+void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
+void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
+                           int32_t nchunks, int32_t ntile, hipStream_t s);  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
                        int izmailov, float c, int32_t L, hipStream_t s);
 void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);

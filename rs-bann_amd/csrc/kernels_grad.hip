@@ -1150,6 +1150,10 @@ __global__ void __launch_bounds__(64 * (NWMAX + 1))
     };
     auto issue_x = [&](int t, auto sc) {
       char* base = xslot(sc);
+#if BANN_ABLATE & 8
+      (void)base;
+      return;  // compute-only profiling build: no genotype traffic
+#endif
 #pragma unroll
       for (int q = 0; q < T; ++q) {
         const int f = min(fbeg + t * T + q, flast);
@@ -1165,7 +1169,9 @@ __global__ void __launch_bounds__(64 * (NWMAX + 1))
       constexpr int s = decltype(sc)::value;
       if (t < ntiles) {
         issue_x(t + D, std::integral_constant<int, (s + D) % R>{});  // clamped: always valid
+#if !(BANN_ABLATE & 8)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T * D) : "memory");  // X(t) landed, X(t+D) in flight
+#endif
         const char* xs = xslot(sc) + lane * 16;
 #pragma unroll
         for (int q = 0; q < T; ++q) {
@@ -1225,19 +1231,371 @@ __global__ void __launch_bounds__(64 * (NWMAX + 1))
   }
 }
 
-// BANN_FUSED_VARIANT: "mx" (default: MFMA backward), "pipe" (VALU backward,
-// dedicated head wave) or "reg" (register-staged lockstep kernel)
+// ---------------------------------------------------------------------------
+// Register-staged variant ("rx", default): the genotype tile goes straight
+// from HBM into VGPRs (global_load_dwordx4, prefetched one tile ahead in a
+// ping-pong register pair; the compiler's counted vmcnt waits keep the next
+// tile in flight), feeds the forward MFMA from registers, and is written to
+// LDS only for the backward's transposed read.  LDS per workgroup is one tile
+// image per chunk wave (32 KiB) plus the partial-Z0 / digit exchange (~20 KiB),
+// so TWO workgroups share a CU: two head waves, two pipelines, 18 waves.
+//
+// U2 = genotypes stored as 2-bit codes in HBM (4x fewer bytes than int8):
+// per (tile of 4 fragments, chunk) a lane holds 4 words, one per fragment;
+// genotype j = 4k + b of the lane's 16 sits at bits 8b + 2k, so byte-group k
+// unpacks as (w >> 2k) & 0x03030303 -- the B operand in two VALU ops per VGPR.
+// Backward-image rows of odd fragments are rotated by 8 rows (128 B), which
+// puts the two 16-lane groups of every transposed read on disjoint banks.
+// ---------------------------------------------------------------------------
+template <int NL, int ACT, bool U2>
+__global__ void __launch_bounds__(576, 6)
+    k_fused_grad_rx(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  constexpr int NW = 8;
+  constexpr int NH = NL - 1;
+  constexpr int T = BANN_TILE_FRAGS;
+  static_assert(T == 4, "the backward MFMA contracts over exactly 4 fragments (64 individuals)");
+  constexpr int DROW = 384;
+  __shared__ __attribute__((aligned(16))) char s_img[NW][T * 1024];
+  __shared__ __attribute__((aligned(16))) float s_zp[2][NW][T][16][4];
+  __shared__ __attribute__((aligned(16))) char s_dig[2][T * DROW];
+  __shared__ __attribute__((aligned(16))) float s_scl[2][4];
+  __shared__ __attribute__((aligned(16))) HeadLds s_hd;
+  __shared__ __attribute__((aligned(16))) float s_db0[4];
+
+  const GradItem it = items[blockIdx.x];
+  const BranchDev& bd = st.br[it.branch];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = bd.nchunks;
+  const int64_t n = st.n;
+  const int fbeg = it.frag_begin, fend = it.frag_end, flast = fend - 1;
+  const int ntiles = (fend - fbeg + T - 1) / T;
+
+  for (int t = threadIdx.x; t < BANN_MAXL * 20; t += blockDim.x) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (l >= 1 && l < NL) {
+      if (r < 16) {
+        const int j = r >> 2, k = r & 3;
+        if (j < bd.win[l] && k < bd.widths[l]) v = st.theta[bd.p_off + bd.woff[l] + k * bd.win[l] + j];
+        s_hd.W[l][j][k] = v;
+      } else {
+        const int k = r - 16;
+        if (l < NL - 1 && k < bd.widths[l]) v = st.theta[bd.p_off + bd.boff[l] + k];
+        s_hd.bias[l][k] = v;
+      }
+    } else if (l == 0 && r >= 16) {
+      const int k = r - 16;
+      s_hd.bias[0][k] = (k < bd.widths[0]) ? st.fc[it.branch].c0[k] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+
+  if (wave == 0) {
+    // ===================== head wave =====================
+    const float* ybr = st.y + bd.y_off;
+    float* predb = st.pred + bd.y_off;
+    auto load_y = [&](int t) -> float {
+      const int64_t row = (int64_t)min(fbeg + t * T + (lane >> 4), flast) * 16 + (lane & 15);
+      return ybr[row < n ? row : n - 1];
+    };
+    double rss = 0.0;
+    float db[NH][4], dWo[4];
+    float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dWo[k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+    }
+    auto head_tile = [&](int t, float yv) {
+      const int q = lane >> 4, rr = lane & 15;
+      const int f = fbeg + t * T + q;
+      const int64_t row = (int64_t)f * 16 + rr;
+      const bool valid = (f < fend) && (row < n);
+      const int zb = t & 1;
+      float d[4];
+#if BANN_ABLATE & 1
+      {
+        const v4f p0 = *reinterpret_cast<const v4f*>(&s_zp[zb][0][q][rr][0]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = valid ? p0[k] * 1e-3f - yv : 0.f;
+      }
+#else
+      float z[NH][4], a[NH][4];
+      v4f zs = *reinterpret_cast<const v4f*>(&s_hd.bias[0][0]);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) zs += *reinterpret_cast<const v4f*>(&s_zp[zb][w][q][rr][0]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[0][k] = zs[k];
+        a[0][k] = act_h_t<ACT>(z[0][k]);
+      }
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float sacc = s_hd.bias[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc = fmaf(a[l - 1][j], s_hd.W[l][j][k], sacc);
+          z[l][k] = sacc;
+          a[l][k] = act_h_t<ACT>(sacc);
+        }
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], s_hd.W[NL - 1][j][0], out);
+      const float e = valid ? out - yv : 0.f;
+      if (write_pred && valid) predb[row] = out;
+      rss += (double)e * (double)e;
+      float err[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+        err[j] = e * s_hd.W[NL - 1][j][0];
+      }
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        float dl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dl[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
+          db[l][k] += dl[k];
+        }
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float sj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dW[l - 1][j][k] = fmaf(a[l - 1][j], dl[k], dW[l - 1][j][k]);
+              sj = fmaf(dl[k], s_hd.W[l][j][k], sj);
+            }
+            err[j] = sj;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = dl[k];
+        }
+      }
+#endif
+      // delta0 -> per-column power-of-two scale + 4 digits (see k_fused_grad_mx)
+      const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+      const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+      const uint32_t E[4] = {e01 & 0xFFFFu, e01 >> 16, e23 & 0xFFFFu, e23 >> 16};
+      v4i w;
+      v4f scl;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = E[k] >= 6u;
+        const float inv = ok ? fpow2(259u - E[k]) : 0.f;
+        scl[k] = ok ? fpow2(E[k] - 5u) : 0.f;
+        w[k] = (int)digits4(d[k] * inv);
+      }
+      *reinterpret_cast<v4i*>(&s_dig[zb][q * DROW + rr * 16]) = w;
+      if (lane == 0) *reinterpret_cast<v4f*>(&s_scl[zb][0]) = scl;
+    };
+    float ya = load_y(0), yb = 0.f;
+    for (int t = 0;; t += 2) {
+      if (t < ntiles) yb = load_y(t + 1);
+      LDS_BARRIER();
+      if (t == ntiles) break;
+      head_tile(t, ya);
+      if (t + 1 < ntiles) ya = load_y(t + 2);
+      LDS_BARRIER();
+      if (t + 1 == ntiles) break;
+      head_tile(t + 1, yb);
+    }
+    const double rs = wave_sum_d(rss);
+    float db0s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db0s[k] = wave_sum(db[0][k]);
+    if (lane == 0) {
+      st.rss_part[(int64_t)it.branch * st.max_splits + it.split] = rs;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s_db0[k] = db0s[k];
+        if (k < bd.widths[0]) part[bd.boff[0] + k] = db0s[k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = wave_sum(dWo[j]);
+      if (lane == 0 && j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = wave_sum(db[l][k]);
+        if (lane == 0 && k < bd.widths[l]) part[bd.boff[l] + k] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float wv = wave_sum(dW[l - 1][j][k]);
+          if (lane == 0 && j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = wv;
+        }
+      }
+    }
+    __syncthreads();  // s_db0 visible to the chunk waves
+  } else {
+    // ===================== chunk waves =====================
+    const int cw = wave - 1;
+    const bool has_chunk = cw < nch;
+    const int mych = has_chunk ? cw : nch - 1;
+    const float scale = has_chunk ? st.fc[it.branch].scale[lane >> 4] : 0.f;  // chunk-less: zp = 0
+    const v4i adig = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)mych * 64 + lane) * 16);
+    // genotype sources (branch-free clamped loads: past the item end re-read its last tile)
+    const int tb0 = fbeg / T, tlast = flast / T;
+    const v4i* xu2 = reinterpret_cast<const v4i*>(st.xu2 + bd.x_off) + (int64_t)mych * 64 + lane;
+    const int8_t* xi8 = st.xpk + bd.x_off + ((int64_t)mych * 64 + lane) * 16;
+    const int64_t frag_bytes = (int64_t)nch * 1024;
+    typedef v4i XReg[U2 ? 1 : T];
+    auto load_tile = [&](int t, XReg& xv) {
+#if BANN_ABLATE & 8
+      // compute-only profiling build: no genotype traffic
+#pragma unroll
+      for (int q = 0; q < (U2 ? 1 : T); ++q) xv[q] = v4i{t, lane, q, 0x01010101};
+      return;
+#endif
+      if constexpr (U2) {
+        xv[0] = xu2[(int64_t)min(tb0 + t, tlast) * nch * 64];
+      } else {
+#pragma unroll
+        for (int q = 0; q < T; ++q)
+          xv[q] = *reinterpret_cast<const v4i*>(xi8 + (int64_t)min(fbeg + t * T + q, flast) * frag_bytes);
+      }
+    };
+    auto unpack = [&](const XReg& xv, v4i (&xu)[T]) {
+      if constexpr (U2) {
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+          const uint32_t wq = (uint32_t)xv[0][q];
+          xu[q] = v4i{(int)(wq & 0x03030303u), (int)((wq >> 2) & 0x03030303u), (int)((wq >> 4) & 0x03030303u),
+                      (int)((wq >> 6) & 0x03030303u)};
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < T; ++q) xu[q] = xv[q];
+      }
+    };
+    char* img = s_img[cw];
+    const int g = lane >> 4, tq = (lane & 15) >> 1, tp = lane & 1;
+    const int rot = 8 * (g & 1);
+    float dw[4] = {0.f, 0.f, 0.f, 0.f};  // dW0 (G^T delta0) of column lane>>4, marker 16u + (lane & 15)
+
+    auto fwd = [&](int t, const v4i (&xu)[T]) {
+#pragma unroll
+      for (int q = 0; q < T; ++q) {
+#if BANN_ABLATE & 4
+        const v4i d = xu[q];
+#else
+        const v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig, xu[q], v4i{0, 0, 0, 0}, 0, 0, 0);
+#endif
+        s_zp[t & 1][cw][q][lane & 15][lane >> 4] =
+            scale * ((float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f);
+      }
+    };
+    auto bwd = [&](int tb) {
+      const char* ds = &s_dig[tb & 1][0] + g * DROW + tq * 16 + 8 * tp;
+      const v4i A = lds_tr8_pair(ds, ds + 8 * 16);
+      const float sc_c = s_scl[tb & 1][g];
+      const char* xs = img + g * 1024 + 8 * tp;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r0 = (16 * u + tq + rot) & 63, r1 = (16 * u + 8 + tq + rot) & 63;
+        const v4i B = lds_tr8_pair(xs + r0 * 16, xs + r1 * 16);
+#if BANN_ABLATE & 2
+        asm volatile("" ::"v"(A), "v"(B));
+#else
+        const v4i gacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B, v4i{0, 0, 0, 0}, 0, 0, 0);
+        const float v =
+            (float)gacc[0] + (float)gacc[1] * 0x1p-7f + (float)gacc[2] * 0x1p-14f + (float)gacc[3] * 0x1p-21f;
+        dw[u] = fmaf(sc_c, v, dw[u]);
+#endif
+      }
+    };
+    auto write_img = [&](const v4i (&xu)[T]) {
+#pragma unroll
+      for (int q = 0; q < T; ++q)
+        *reinterpret_cast<v4i*>(img + q * 1024 + ((lane + 8 * (q & 1)) & 63) * 16) = xu[q];
+    };
+
+    XReg xa, xb;
+    load_tile(0, xa);
+    for (int t = 0;; t += 2) {
+      v4i xu[T];
+      if (t < ntiles) {
+        load_tile(t + 1, xb);
+        unpack(xa, xu);
+        fwd(t, xu);
+      }
+      LDS_BARRIER();
+      if (t >= 1 && has_chunk) bwd(t - 1);
+      if (t == ntiles) break;
+      write_img(xu);
+
+      v4i xv[T];
+      if (t + 1 < ntiles) {
+        load_tile(t + 2, xa);
+        unpack(xb, xv);
+        fwd(t + 1, xv);
+      }
+      LDS_BARRIER();
+      if (has_chunk) bwd(t);
+      if (t + 1 == ntiles) break;
+      write_img(xv);
+    }
+    __syncthreads();  // s_db0 published by the head wave
+    if (has_chunk) {
+      const int c = lane >> 4;
+      if (c < bd.widths[0]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int sidx = cw * 64 + u * 16 + (lane & 15);
+          if (sidx < bd.m) {
+            const float mu = st.mu[bd.mk_off + sidx], sg = st.sigma[bd.mk_off + sidx];
+            part[bd.woff[0] + c * bd.m + sidx] = sg > 0.f ? (dw[u] - mu * s_db0[c]) / sg : 0.f;
+          }
+        }
+      }
+    }
+  }
+}
+
+// BANN_FUSED_VARIANT: "rx" (default: register-staged, MFMA backward, 2 WG/CU),
+// "mx" (LDS-DMA ring, MFMA backward), "pipe" (LDS-DMA ring, VALU backward) or
+// "reg" (register-staged lockstep, VALU backward).  BANN_GENO_FORMAT = "u2"
+// (default for rx: 2-bit genotype codes in HBM) or "i8".
 static int fused_variant() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("BANN_FUSED_VARIANT");
-    v = (e && e[0] == 'p') ? 2 : (e && e[0] == 'r') ? 0 : 3;
+    if (!e || !e[0] || (e[0] == 'r' && e[1] == 'x')) v = 4;
+    else if (e[0] == 'm') v = 3;
+    else if (e[0] == 'p') v = 2;
+    else v = 0;
   }
   return v;
 }
 
+int fused_prefers_u2() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("BANN_GENO_FORMAT");
+    u = (fused_variant() == 4 && !(e && e[0] == 'i')) ? 1 : 0;
+  }
+  return u;
+}
+
 const char* fused_kernel_family() {
   switch (fused_variant()) {
+    case 4: return "k_fused_grad_rx";
     case 3: return "k_fused_grad_mx";
     case 2: return "k_fused_grad_pipe";
     default: return "k_fused_grad";
@@ -1247,6 +1605,13 @@ const char* fused_kernel_family() {
 template <int NL, int ACT>
 static void launch_fused_t(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int wp,
                            hipStream_t s) {
+  if (fused_variant() == 4 && nwaves <= 8) {
+    if (st.u2)
+      hipLaunchKernelGGL((k_fused_grad_rx<NL, ACT, true>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
+    else
+      hipLaunchKernelGGL((k_fused_grad_rx<NL, ACT, false>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
+    return;
+  }
   if (fused_variant() == 3 && nwaves <= 8) {
     hipLaunchKernelGGL((k_fused_grad_mx<NL, 8, ACT>), dim3(nitems), dim3(64 * 9), 0, s, st, items, wp);
     return;

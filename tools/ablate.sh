@@ -1,9 +1,11 @@
 #!/bin/bash
-# run the kernel micro-benchmark over kernel variants and ablation builds (profiling only)
+# kernel micro-benchmark over the fused-kernel variants and the ablation builds
+# (make -C rs-bann_amd/csrc ablate first; profiling only)
 set -e
 ARGS="$@"
-timeout -k 10 120 python tools/kbench.py $ARGS --tag pipe
-BANN_FUSED_VARIANT=reg timeout -k 10 120 python tools/kbench.py $ARGS --tag reg
-for a in 1 2 3; do
-  BANN_LIB=rs-bann_amd/abl/librsbann_amd_abl$a.so timeout -k 10 120 python tools/kbench.py $ARGS --tag pipe_abl$a
+for v in mx pipe reg; do
+  BANN_FUSED_VARIANT=$v timeout -k 10 120 python tools/kbench.py $ARGS --tag $v
+done
+for a in 1 2 4 3 7 8 15; do
+  BANN_LIB=rs-bann_amd/abl/librsbann_amd_abl$a.so timeout -k 10 120 python tools/kbench.py $ARGS --tag mx_abl$a
 done
