@@ -682,7 +682,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8)
+    if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8 && fused_u2_layout())
+      launch_pack_branch_u2t(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
+                             ctx->stream);
+    else if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8)
       launch_pack_branch_u2(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
                             ctx->stream);
     else

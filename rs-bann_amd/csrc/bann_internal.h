@@ -115,10 +115,15 @@ void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb,
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
 const char* fused_kernel_family();
-int fused_prefers_u2();             // the fused variant reads 2-bit genotypes unless BANN_GENO_FORMAT=i8
+int fused_prefers_u2();
+int fused_u2_layout();              // 1: fx tile-row image (launch_pack_branch_u2t), 0: rx image             // the fused variant reads 2-bit genotypes unless BANN_GENO_FORMAT=i8
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
                            int32_t nchunks, int32_t ntile, hipStream_t s);  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
+void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
+                          int write_pred, hipStream_t s);
+void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
+                            int32_t nchunks, int32_t ntile, hipStream_t s);
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
                        int izmailov, float c, int32_t L, hipStream_t s);
 void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);

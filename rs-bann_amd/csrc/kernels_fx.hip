@@ -1,0 +1,492 @@
+// kernels_fx.hip — the "fx" fused gradient kernel (default): one WAVE owns a
+// 64-individual tile of one branch across ALL of its marker chunks.
+//
+// Replaces BranchSampler::backpropagate (branch_sampler.rs:813-875) with its
+// forward_feed (743-782) and the rss it stores (823-828), for every branch of a
+// plan in one launch, and writes the same per-split partial slabs as the other
+// fused variants (d(rss/2)/d(theta) in param_vec order, params.rs:700-715).
+//
+// Why this shape (measured on the chunk-wave kernels it replaces): with one
+// wave per 64-marker chunk, every tile needs a cross-wave exchange of partial
+// Z0 and of delta0 (two barriers), the per-individual head serialises on one
+// wave, and every MFMA result is converted to f32 on its own -- issue- and
+// latency-bound at 2.4 TB/s of 2-bit genotypes.  Here:
+//   * the forward accumulates Z0 over all chunks in the MFMA's int32
+//     accumulator (exact), converted once per tile;
+//   * the head runs in every wave, one individual per lane;
+//   * dW0 = G^T delta0 accumulates over ALL tiles of the item in int32 digit
+//     sums with a per-column running power-of-two scale (rescaled exactly by
+//     digit carry in the rare case a tile's |delta0| outgrows it), converted to
+//     f32 once at the end;
+//   * waves never wait for each other inside the tile loop: each streams its
+//     own tiles into its own LDS slots (LDS-DMA, one tile ahead, counted
+//     vmcnt) -- the only barriers are the final workgroup reduction.
+//
+// Genotype tile image (HBM == LDS, 16 B per marker row, "u2t" layout):
+//   row j (marker) = 16 quads Q; quad Q = individuals 4Q .. 4Q+3 as 2-bit
+//   codes at bits 2p (p = individual - 4Q).  Rows are stored in 16-row windows
+//   w = j >> 4 at position P = ((j & 15) + 8 (w & 1)) & 15, and the two 8-byte
+//   halves of a row at position P >= 8 are swapped (bank-conflict-free reads).
+//   * forward B operand (K = 64 markers, N = 16 individuals): two
+//     ds_read_b64_tr_b8 per chunk give lane (g, i) the quad-i byte of the 16
+//     markers of window 4c + g; (x >> 2q) & 0x03030303 is the i8 operand of
+//     individual 4i + q ("fragment" q).
+//   * backward B operand (K = 64 individuals, N = 16 markers): one ds_read_b32
+//     gives lane (r, n) quads 4r .. 4r+3 of marker 16u + n; (w >> 2p) &
+//     0x03030303 holds individuals 16r + 4b + p (byte b), K slot 16r + 4p + b.
+//     The delta0 digit operand A is written in the same K order.
+#include <stdlib.h>
+
+#include "activations.h"
+#include "bann_internal.h"
+#include "kernel_util.h"
+
+#define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
+#define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
+#define FX_DROW 384       // delta0 digit image: 16 rows x 16 B + 128 B bank padding per K group
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float ufl(float v) {  // make a wave-uniform value scalar
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
+// all but the youngest k vector-memory operations of this wave are complete
+__device__ __forceinline__ void vm_wait(int k) {
+  switch (k) {
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ float comb4(v4i d) {  // sum_d D_d 2^(-7 d)
+  return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
+}
+
+// value(G) * 2^-sh for digit sums G (digit d weighs 2^(-7 d)), 0 <= sh <= 7:
+// floor-shift each digit and carry its remainder into the next one (exact up
+// to the dropped remainder of the last digit, < 2^-21 of the new unit).
+__device__ __forceinline__ v4i shr_digits(v4i G, int sh) {
+  const int cs = 7 - sh;
+  const int g0 = G[0] >> sh, r0 = G[0] - (g0 << sh);
+  const int t1 = G[1] + (r0 << cs), g1 = t1 >> sh, r1 = t1 - (g1 << sh);
+  const int t2 = G[2] + (r1 << cs), g2 = t2 >> sh, r2 = t2 - (g2 << sh);
+  const int t3 = G[3] + (r2 << cs), g3 = t3 >> sh;
+  return v4i{g0, g1, g2, g3};
+}
+
+// signed digits of V = rint(v 2^21), |v| < 64:  V = d0 2^21 + d1 2^14 + d2 2^7 + d3,
+// d0 in [-64, 64], d1..d3 in [0, 127]; packed little-endian (byte d = digit d)
+__device__ __forceinline__ uint32_t digits4_fx(float x, int e) {
+  const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
+  const uint32_t u = (uint32_t)V;
+  uint32_t w = __builtin_amdgcn_ubfe(u, 21, 8);
+  w |= __builtin_amdgcn_ubfe(u, 14, 7) << 8;
+  w |= __builtin_amdgcn_ubfe(u, 7, 7) << 16;
+  w |= (u & 127u) << 24;
+  return w;
+}
+
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                                  false, false);
+  a = __builtin_bit_cast(float, (unsigned)r[0]);
+  b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ void swap16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b),
+                                                  false, false);
+  a = __builtin_bit_cast(float, (unsigned)r[0]);
+  b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+template <int NL, int ACT>
+__global__ void __launch_bounds__(64 * FX_WAVES, 2)
+    k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  constexpr int NH = NL - 1;  // layers with activations
+  constexpr int NW = FX_WAVES;
+  constexpr int NS = 8 + (NH - 1) * 20;  // head statistics per wave
+  __shared__ __attribute__((aligned(16))) char s_x[NW][2][FX_SLOT];
+  __shared__ __attribute__((aligned(16))) char s_dig[NW][4 * FX_DROW];
+  __shared__ __attribute__((aligned(16))) float s_y[NW][2][64];
+  __shared__ float s_hs[NW][NS];
+  __shared__ double s_rss[NW];
+
+  const GradItem it = items[blockIdx.x];
+  const int b = it.branch;
+  const BranchDev& bd = st.br[b];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = bd.nchunks;
+  const int64_t n = st.n;
+  const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
+
+  // ---- branch constants: head weights (uniform, scalar), W0 digits, column scale ----
+  const float* th = st.theta + bd.p_off;
+  float Wh[NL][4][4];  // Wh[l][j][k] = W_l[j][k] (l >= 1), zero padded to 4 x 4
+  float Bh[NH][4];     // Bh[0] = c0 (folded standardisation), Bh[l] = b_l
+#pragma unroll
+  for (int l = 1; l < NL; ++l)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v = 0.f;
+        if (j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+        Wh[l][j][k] = ufl(v);
+      }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    Bh[0][k] = ufl(k < bd.widths[0] ? st.fc[b].c0[k] : 0.f);
+#pragma unroll
+    for (int l = 1; l < NH; ++l) Bh[l][k] = ufl(k < bd.widths[l] ? th[bd.boff[l] + k] : 0.f);
+  }
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
+  float zscale = st.fc[b].scale[g];
+  v4i adig[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+    adig[c] = c < nch ? *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16)
+                      : v4i{0, 0, 0, 0};
+  // retire the prologue loads and hide their provenance: inside the tile loop the
+  // only vector-memory waits are the explicit, counted ones on this wave's DMAs
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(adig[c]));
+  asm volatile("" : "+v"(zscale));
+
+  // ---- per-lane LDS offsets ----
+  const int gsw = g & 1;
+  const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
+  const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
+  const int pe = i16, po = (i16 + 8) & 15;
+  const uint32_t boe = (uint32_t)(pe * 16 + 4 * (2 * ((g >> 1) ^ (pe >> 3)) + (g & 1)));
+  const uint32_t boo = (uint32_t)(po * 16 + 4 * (2 * ((g >> 1) ^ (po >> 3)) + (g & 1)));
+  const int iota = 4 * i16 + g;  // individual of this lane in the head (after the transpose)
+  char* const sd = &s_dig[wave][0];
+  char* const sd_w = sd + (i16 >> 2) * FX_DROW + (4 * g + (i16 & 3)) * 16;  // row K(iota)
+  const char* const sd_r = sd + g * FX_DROW + tq * 16 + 8 * tp;
+  const float* ybr = st.y + bd.y_off;
+  float* predb = st.pred + bd.y_off;
+  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
+  const int64_t tile_bytes = (int64_t)nch * 1024;
+
+  auto issue = [&](int tt, int sl) {
+    const char* src = xsrc + (int64_t)tt * tile_bytes;
+    char* dst = &s_x[wave][sl][0];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (c < nch) glds16(src + c * 1024, dst + c * 1024);
+    const int64_t row = 64 * (int64_t)tt + iota;
+    glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
+  };
+
+  // ---- accumulators ----
+  v4i acc[32];  // dW0 digit sums per 16-marker window u (lane: column g, marker 16u + i16)
+#pragma unroll
+  for (int u = 0; u < 32; ++u) acc[u] = v4i{0, 0, 0, 0};
+  int R[4] = {0, 0, 0, 0};  // running delta0 scale exponent per column (0 = unset)
+  double rss = 0.0;
+  float db[NH][4], dWo[4];
+  float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dWo[k] = 0.f;
+#pragma unroll
+    for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+    for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+  }
+
+  int tt = tb + wave, sl = 0;
+  if (tt < te) issue(tt, 0);
+  for (; tt < te; tt += NW, sl ^= 1) {
+    const bool more = tt + NW < te;
+    if (more) issue(tt + NW, sl ^ 1);
+    vm_wait(more ? nch + 1 : 0);
+    const char* xs = &s_x[wave][sl][0];
+
+    // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
+    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      if (c < nch) {
+        const v4u X = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const v4i Bq = (v4i)((X >> (2u * q)) & 0x03030303u);
+#if BANN_ABLATE & 4
+          facc[q] += Bq;
+#else
+          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig[c], Bq, facc[q], 0, 0, 0);
+#endif
+        }
+      }
+    }
+    // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
+    // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
+    float z0 = zscale * comb4(facc[0]), z1 = zscale * comb4(facc[1]);
+    float z2 = zscale * comb4(facc[2]), z3 = zscale * comb4(facc[3]);
+    swap32(z0, z2);
+    swap32(z1, z3);
+    swap16(z0, z1);
+    swap16(z2, z3);
+
+    // ---- head: one individual per lane ----
+    const int64_t row = 64 * (int64_t)tt + iota;
+    const bool valid = row < n;
+    const float yv = s_y[wave][sl][lane];
+    float d[4];
+    {
+      float z[NH][4], a[NH][4];
+      z[0][0] = z0 + Bh[0][0];
+      z[0][1] = z1 + Bh[0][1];
+      z[0][2] = z2 + Bh[0][2];
+      z[0][3] = z3 + Bh[0][3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[0][k] = act_h_t<ACT>(z[0][k]);
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float s = Bh[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s = fmaf(a[l - 1][j], Wh[l][j][k], s);
+          z[l][k] = s;
+          a[l][k] = act_h_t<ACT>(s);
+        }
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], Wh[NL - 1][j][0], out);
+      const float e = valid ? out - yv : 0.f;
+      if (write_pred && valid) predb[row] = out;
+      rss += (double)e * (double)e;
+      float err[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+        err[j] = e * Wh[NL - 1][j][0];
+      }
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        float dl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dl[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
+          db[l][k] += dl[k];
+        }
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float sj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dW[l - 1][j][k] = fmaf(a[l - 1][j], dl[k], dW[l - 1][j][k]);
+              sj = fmaf(dl[k], Wh[l][j][k], sj);
+            }
+            err[j] = sj;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = dl[k];
+        }
+      }
+    }
+
+    // ---- delta0 -> signed digits at the running per-column scale 2^(R - 132) ----
+    const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+    const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+    const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
+    int dl[4];
+    bool grow = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dl[k] = 0;
+      if (E[k] >= 6 && (R[k] == 0 || E[k] > R[k])) {  // first scale, or |delta| outgrew it
+        if (R[k] != 0) {
+          dl[k] = E[k] + 2 - R[k];
+          grow = true;
+        }
+        R[k] = E[k] + 2;
+      }
+    }
+    if (grow) {  // rare: rescale the digit sums of the grown columns exactly
+      int rem = g == 0 ? dl[0] : g == 1 ? dl[1] : g == 2 ? dl[2] : dl[3];
+      while (__builtin_amdgcn_ballot_w64(rem > 0) != 0) {
+        const int sh = rem < 7 ? rem : 7;
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          if (u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
+        rem -= sh;
+      }
+    }
+    v4u w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - (R[k] ? R[k] : 255));
+    *reinterpret_cast<v4u*>(sd_w) = w;
+
+    // ---- backward: dW0 digit sums += G^T delta0 ----
+    const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      if (u < 4 * nch) {
+        const uint32_t wv = *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe));
+        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u),
+                           (int)((wv >> 4) & 0x03030303u), (int)((wv >> 6) & 0x03030303u)};
+#if BANN_ABLATE & 2
+        acc[u] += Bv ^ A;
+#else
+        acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
+#endif
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- workgroup reduction (fixed order: deterministic) ----
+  {
+    const double rs = wave_sum_d(rss);
+    float hs[NS];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hs[k] = wave_sum(db[0][k]);
+      hs[4 + k] = wave_sum(dWo[k]);
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hs[8 + (l - 1) * 20 + k] = wave_sum(db[l][k]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hs[8 + (l - 1) * 20 + 4 + 4 * j + k] = wave_sum(dW[l - 1][j][k]);
+      }
+    if (lane == 0) {
+      s_rss[wave] = rs;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) s_hs[wave][q] = hs[q];
+    }
+  }
+  __syncthreads();  // every wave is done with its tile slots
+  {
+    const int Rl = g == 0 ? R[0] : g == 1 ? R[1] : g == 2 ? R[2] : R[3];
+    float* red = reinterpret_cast<float*>(&s_x[wave][0][0]);
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4(acc[u]), Rl - 132) : 0.f;
+  }
+  __syncthreads();
+  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+  float db0[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) db0[k] = (s_hs[0][k] + s_hs[1][k]) + (s_hs[2][k] + s_hs[3][k]);
+  const int m = bd.m;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int u = wave * 8 + jj;
+    if (u < 4 * nch) {
+      const int idx = u * 64 + lane;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += reinterpret_cast<const float*>(&s_x[w][0][0])[idx];
+      const int mk = 16 * u + i16, c = g;
+      if (mk < m && c < bd.widths[0]) {
+        const float mu = st.mu[bd.mk_off + mk], sg = st.sigma[bd.mk_off + mk];
+        const float dbc = c == 0 ? db0[0] : c == 1 ? db0[1] : c == 2 ? db0[2] : db0[3];
+        part[bd.woff[0] + c * m + mk] = sg > 0.f ? (s - mu * dbc) / sg : 0.f;
+      }
+    }
+  }
+  if (wave == 0 && lane < NS) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_hs[w][lane];
+    const int q = lane;
+    if (q < 4) {
+      if (q < bd.widths[0]) part[bd.boff[0] + q] = v;
+    } else if (q < 8) {
+      const int j = q - 4;
+      if (j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+    } else {
+      const int l = 1 + (q - 8) / 20, r = (q - 8) % 20;
+      if (r < 4) {
+        if (r < bd.widths[l]) part[bd.boff[l] + r] = v;
+      } else {
+        const int j = (r - 4) >> 2, k = (r - 4) & 3;
+        if (j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = v;
+      }
+    }
+  }
+  if (wave == 0 && lane == 0)
+    st.rss_part[(int64_t)b * st.max_splits + it.split] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
+}
+
+template <int NL>
+static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
+  switch (act) {
+    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0>), grid, block, 0, s, st, items, wp); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1>), grid, block, 0, s, st, items, wp); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2>), grid, block, 0, s, st, items, wp); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3>), grid, block, 0, s, st, items, wp); break;
+    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4>), grid, block, 0, s, st, items, wp); break;
+  }
+}
+
+void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
+                          int write_pred, hipStream_t s) {
+  if (nitems <= 0) return;
+  switch (L) {
+    case 2: launch_fx_nl<2>(st, items, nitems, act, write_pred, s); break;
+    case 3: launch_fx_nl<3>(st, items, nitems, act, write_pred, s); break;
+    case 4: launch_fx_nl<4>(st, items, nitems, act, write_pred, s); break;
+    default: break;
+  }
+}
+
+// ---- "u2t" tile-row genotype image (see the header comment) ----
+__global__ void k_pack_u2t(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,
+                           uint8_t* __restrict__ dst, int32_t nchunks, int32_t ntile) {
+  const int rows = 64 * nchunks;
+  const int64_t total = (int64_t)ntile * rows;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % rows);
+    const int64_t tile = t / rows;
+    uint8_t q[16];
+#pragma unroll
+    for (int Q = 0; Q < 16; ++Q) {
+      uint32_t v = 0;
+      if (j < m) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int64_t row = 64 * tile + 4 * Q + p;
+          if (row < n) v |= ((uint32_t)g[(int64_t)idx[j] * n + row] & 3u) << (2 * p);
+        }
+      }
+      q[Q] = (uint8_t)v;
+    }
+    const int w = j >> 4, P = ((j & 15) + 8 * (w & 1)) & 15, sw = P >> 3;
+    uint8_t* o = dst + tile * (int64_t)rows * 16 + (16 * w + P) * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int bq = 0; bq < 8; ++bq) o[8 * (h ^ sw) + bq] = q[8 * h + bq];
+  }
+}
+
+void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
+                            int32_t nchunks, int32_t ntile, hipStream_t s) {
+  const int64_t total = (int64_t)ntile * 64 * nchunks;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(k_pack_u2t, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, g, snp_idx, m, n,
+                     dst, nchunks, ntile);
+}

@@ -25,9 +25,8 @@
 #include <type_traits>
 
 #include "bann_internal.h"
+#include "kernel_util.h"
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef float v4f __attribute__((ext_vector_type(4)));
 
 // Ablation switches for profiling builds only (make ABLATE=n): 1 = skip the head,
 // 2 = skip the VALU backward, 4 = skip the MFMA forward.  0 in every shipped build.
@@ -186,23 +185,6 @@ void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb
 // ===========================================================================
 // fused path
 // ===========================================================================
-// LDS image of one branch's head parameters, padded to 4x4 (zeros outside the
-// real widths, so padded units stay exactly 0 and contribute nothing).
-struct HeadLds {
-  float W[BANN_MAXL][4][4];  // W_l[j][k], l >= 1
-  float bias[BANN_MAXL][4];  // b_l (l >= 1), c0 for l = 0
-};
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // One work item = fragments [frag_begin, frag_end) of one branch.  Wave w owns
 // marker chunk w for the whole item: its A operand (W0/sigma digits) and its
@@ -491,37 +473,6 @@ __global__ void __launch_bounds__(64 * NWMAX) k_fused_grad(DevState st, const Gr
   }
 }
 
-#define LDS_BARRIER()                                      \
-  do {                                                     \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");     \
-    __builtin_amdgcn_s_barrier();                          \
-    asm volatile("" ::: "memory");                         \
-  } while (0)
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-// LDS stores issued through inline asm: hipcc's wait-count pass does not see
-// them, so it does not drain in-flight LDS-DMA (vmcnt(0)) in front of every
-// store as it does for a ds_write it cannot disambiguate from the DMA target.
-// Their completion is ordered by the explicit lgkmcnt(0) of LDS_BARRIER.
-__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
-// LDS-DMA through inline asm as well: the wave's own counted "s_waitcnt vmcnt"
-// (explicit, below) is then the only wait on it.  M0 = wave-uniform LDS base;
-// the data lands at M0 + 16 * lane (4 * lane for the dword form).
-__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");
-}
-__device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");
-}
-__device__ __forceinline__ void lds_st_f32(float* p, float v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
-}
-__device__ __forceinline__ void lds_st_v4f(v4f* p, v4f v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(lds_off(p)), "v"(v) : "memory");
-}
 
 // ---------------------------------------------------------------------------
 // Pipelined variant (default): wave 0 is a dedicated HEAD wave, waves 1..NW own
@@ -876,43 +827,6 @@ __global__ void __launch_bounds__(64 * (NWMAX + 1))
 // The fragment stride in LDS is padded to 1152 B (and 384 B in the digit
 // image) so the two 16-lane groups of a half-wave read disjoint bank halves.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t fbits(float x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ float fpow2(uint32_t biased_exp) { return __builtin_bit_cast(float, biased_exp << 23); }
-
-typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t max_u16x2(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(v2u16, a), __builtin_bit_cast(v2u16, b)));
-}
-// wave-wide max of two packed u16 lanes (DPP row reductions, result uniform)
-__device__ __forceinline__ uint32_t wave_max_u16x2(uint32_t v) {
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false));  // row_mirror
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast15
-  v = max_u16x2(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-typedef int v2i __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) v2i lds_v2i;
-__device__ __forceinline__ v4i lds_tr8_pair(const char* p0, const char* p1) {
-  const v2i a = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p0));
-  const v2i b = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(p1));
-  return v4i{a.x, a.y, b.x, b.y};
-}
-
-// four signed 7-bit digits of v (|v| < 64), most significant first, packed LE
-__device__ __forceinline__ uint32_t digits4(float v) {
-  uint32_t w = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const float r = __builtin_rintf(v);
-    w |= ((uint32_t)(int)r & 0xFFu) << (8 * d);
-    v = (v - r) * 128.f;
-  }
-  return w;
-}
 
 template <int NL, int NWMAX, int ACT>
 __global__ void __launch_bounds__(64 * (NWMAX + 1))
@@ -1568,15 +1482,17 @@ __global__ void __launch_bounds__(576, 6)
   }
 }
 
-// BANN_FUSED_VARIANT: "rx" (default: register-staged, MFMA backward, 2 WG/CU),
-// "mx" (LDS-DMA ring, MFMA backward), "pipe" (LDS-DMA ring, VALU backward) or
-// "reg" (register-staged lockstep, VALU backward).  BANN_GENO_FORMAT = "u2"
-// (default for rx: 2-bit genotype codes in HBM) or "i8".
+// BANN_FUSED_VARIANT: "fx" (default: wave-per-tile, int32 accumulation over
+// chunks and tiles, kernels_fx.hip), "rx" (register-staged, MFMA backward,
+// 2 WG/CU), "mx" (LDS-DMA ring, MFMA backward), "pipe" (LDS-DMA ring, VALU
+// backward) or "reg" (register-staged lockstep, VALU backward).
+// BANN_GENO_FORMAT = "u2" (default for fx / rx: 2-bit genotype codes in HBM) or "i8".
 static int fused_variant() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("BANN_FUSED_VARIANT");
-    if (!e || !e[0] || (e[0] == 'r' && e[1] == 'x')) v = 4;
+    if (!e || !e[0] || (e[0] == 'f' && e[1] == 'x')) v = 5;
+    else if (e[0] == 'r' && e[1] == 'x') v = 4;
     else if (e[0] == 'm') v = 3;
     else if (e[0] == 'p') v = 2;
     else v = 0;
@@ -1588,13 +1504,16 @@ int fused_prefers_u2() {
   static int u = -1;
   if (u < 0) {
     const char* e = getenv("BANN_GENO_FORMAT");
-    u = (fused_variant() == 4 && !(e && e[0] == 'i')) ? 1 : 0;
+    u = (fused_variant() >= 4 && !(e && e[0] == 'i')) ? 1 : 0;
   }
   return u;
 }
 
+int fused_u2_layout() { return fused_variant() == 5 ? 1 : 0; }
+
 const char* fused_kernel_family() {
   switch (fused_variant()) {
+    case 5: return "k_fused_grad_fx";
     case 4: return "k_fused_grad_rx";
     case 3: return "k_fused_grad_mx";
     case 2: return "k_fused_grad_pipe";
@@ -1641,6 +1560,10 @@ static void launch_fused_nl(const DevState& st, const GradItem* items, int32_t n
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
                        int32_t act, int write_pred, hipStream_t s) {
   if (nitems <= 0) return;
+  if (fused_variant() == 5 && st.u2 && nwaves <= 8) {
+    launch_fused_grad_fx(st, items, nitems, L, act, write_pred, s);
+    return;
+  }
   switch (L) {
     case 2: launch_fused_nl<2>(st, items, nitems, nwaves, act, write_pred, s); break;
     case 3: launch_fused_nl<3>(st, items, nitems, nwaves, act, write_pred, s); break;

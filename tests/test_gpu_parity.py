@@ -397,3 +397,60 @@ def test_error_paths(Ctx):
     with pytest.raises(BannError):
         ctx.add_branch([0], [1, 1])                         # after finalize
     ctx.close()
+
+
+# ------------------------------------------------ fx kernel specifics
+def test_default_fused_kernel_is_fx(Ctx):
+    """The product path is the wave-per-tile kernel on 2-bit genotypes."""
+    rng, g, snps, br = make_problem(dict(n=300, m=100, widths=[4, 4, 1], act="tanh", prior="ridge_ard"), 5)
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=rng.normal(size=300))])
+    assert ctx.kernel_path(0) == "fused"
+    assert ctx.fused_kernel_name() == "k_fused_grad_fx"
+    # 2-bit image: ceil(n / 64) tiles x ceil(m / 64) chunks x 1 KiB
+    assert ctx.packed_genotype_bytes == ((300 + 63) // 64) * ((100 + 63) // 64) * 1024
+    ctx.close()
+
+
+@pytest.mark.parametrize("growth", [1.0, 300.0, 1e5])
+def test_delta_scale_growth(Ctx, growth):
+    """delta0 grows along the individuals (later tiles have residuals up to
+    `growth` x larger): the kernel's running per-column digit scale must be
+    rescaled exactly (shr_digits) -- parity with the oracle at every growth."""
+    n, m = 6000, 320
+    rng, g, snps, br = make_problem(dict(n=n, m=m, widths=[4, 4, 1], act="tanh", prior="ridge_ard"), 11)
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(n))])
+    X = oracle_inputs(ctx, g, snps)
+    f = O.predict(br, X)
+    ramp = np.exp(np.linspace(0.0, np.log(growth), n)) if growth > 1 else np.ones(n)
+    y = (f + ramp * rng.normal(size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    grad, rss = ctx.log_density_gradient(0)
+    ogw, ogb, orss = O.log_density_gradient(br, X, y)
+    gw, gb = layer_views(br, grad)
+    for l in range(br.num_layers):
+        assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
+    for l in range(br.num_layers - 1):
+        assert norm_rel(gb[l], ogb[l]) < TOL, ("b", l, norm_rel(gb[l], ogb[l]))
+    assert scalar_close(rss, orss), (rss, orss)
+    ctx.close()
+
+
+def test_c3_shape_branch_parity(Ctx):
+    """One branch of the bench cohort's shape (n = 50 000, m = 500, W = S = 4):
+    782 tiles over many work items and all four waves of each."""
+    n, m = 50_000, 500
+    rng, g, snps, br = make_problem(dict(n=n, m=m, widths=[4, 4, 1], act="tanh", prior="ridge_ard"), 21)
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(n))])
+    X = oracle_inputs(ctx, g, snps)
+    f = O.predict(br, X)
+    y = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    grad, rss = ctx.log_density_gradient(0)
+    ogw, ogb, orss = O.log_density_gradient(br, X, y)
+    assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL
+    gw, gb = layer_views(br, grad)
+    for l in range(br.num_layers):
+        assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
+    assert scalar_close(rss, orss), (rss, orss)
+    assert norm_rel(ctx.predict(0), f) < TOL
+    ctx.close()
