@@ -259,7 +259,7 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       p.max_p_generic = std::max(p.max_p_generic, h.P);
       continue;
     }
-    const int grp = ((h.L - 2) * 5 + h.act) * 2 + (h.dev.nchunks > 8 ? 1 : 0);
+    const int grp = ((h.L - 2) * 5 + h.act) * 3 + (h.dev.nchunks < 8 ? 0 : h.dev.nchunks == 8 ? 1 : 2);
     const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
     const int ns = h.dev.nsplits;
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
@@ -310,8 +310,8 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
   for (int g = 0; g < BANN_NGROUPS; ++g)
     if (!p.items[g].empty())
-      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 10 + 2, (g / 2) % 5,
-                        write_pred, ctx->stream);
+      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 15 + 2, (g / 3) % 5,
+                        g % 3 == 1, write_pred, ctx->stream);
   if (!p.generic.empty())
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
   CK(hipGetLastError());

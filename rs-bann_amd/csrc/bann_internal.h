@@ -105,8 +105,9 @@ void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp
                          float* sig_b, hipStream_t s);
 
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
-                       int32_t act, int write_pred, hipStream_t s);
-#define BANN_NGROUPS 30  // fused launch groups: ((L - 2) * 5 + activation) * 2 + (nchunks > 8), L in [2, 4]
+                       int32_t act, int full8, int write_pred, hipStream_t s);
+// fused launch groups: ((L - 2) * 5 + activation) * 3 + (nchunks < 8 ? 0 : nchunks == 8 ? 1 : 2), L in [2, 4]
+#define BANN_NGROUPS 45
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
@@ -121,7 +122,7 @@ void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_
 void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
                            int32_t nchunks, int32_t ntile, hipStream_t s);  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int write_pred, hipStream_t s);
+                          int full8, int write_pred, hipStream_t s);
 void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
                             int32_t nchunks, int32_t ntile, hipStream_t s);
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,

@@ -43,7 +43,7 @@
 
 #define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
 #define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
-#define FX_DROW 384       // delta0 digit image: 16 rows x 16 B + 128 B bank padding per K group
+#define FX_DROW 256       // delta0 digit image: 16 rows x 16 B per K group (read twice per tile)
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -70,16 +70,14 @@ __device__ __forceinline__ float comb4(v4i d) {  // sum_d D_d 2^(-7 d)
   return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
 }
 
-// value(G) * 2^-sh for digit sums G (digit d weighs 2^(-7 d)), 0 <= sh <= 7:
-// floor-shift each digit and carry its remainder into the next one (exact up
-// to the dropped remainder of the last digit, < 2^-21 of the new unit).
+// value(G) * 2^-sh for digit sums G (digit d weighs 2^(-7 d)), sh >= 0: form
+// N = G0 2^21 + G1 2^14 + G2 2^7 + G3 in int64 (|G_d| < 2^24), shift it, and
+// re-split into 7-bit digits (exact up to the dropped low bits, < 2^-21 of the
+// new unit).  Branch- and loop-free so the accumulators are updated in place.
 __device__ __forceinline__ v4i shr_digits(v4i G, int sh) {
-  const int cs = 7 - sh;
-  const int g0 = G[0] >> sh, r0 = G[0] - (g0 << sh);
-  const int t1 = G[1] + (r0 << cs), g1 = t1 >> sh, r1 = t1 - (g1 << sh);
-  const int t2 = G[2] + (r1 << cs), g2 = t2 >> sh, r2 = t2 - (g2 << sh);
-  const int t3 = G[3] + (r2 << cs), g3 = t3 >> sh;
-  return v4i{g0, g1, g2, g3};
+  const int64_t N = ((int64_t)G[0] << 21) + ((int64_t)G[1] << 14) + ((int64_t)G[2] << 7) + (int64_t)G[3];
+  const int64_t M = N >> (sh < 63 ? sh : 63);
+  return v4i{(int)(M >> 21), (int)((M >> 14) & 127), (int)((M >> 7) & 127), (int)(M & 127)};
 }
 
 // signed digits of V = rint(v 2^21), |v| < 64:  V = d0 2^21 + d1 2^14 + d2 2^7 + d3,
@@ -107,8 +105,10 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
   b = __builtin_bit_cast(float, (unsigned)r[1]);
 }
 
-template <int NL, int ACT>
-__global__ void __launch_bounds__(64 * FX_WAVES, 2)
+// NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
+// so the LDS reads of a whole phase issue back to back); 0 = any count <= 8.
+template <int NL, int ACT, int NCH>
+__global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred) {
   constexpr int NH = NL - 1;  // layers with activations
   constexpr int NW = FX_WAVES;
@@ -116,6 +116,8 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
   __shared__ __attribute__((aligned(16))) char s_x[NW][2][FX_SLOT];
   __shared__ __attribute__((aligned(16))) char s_dig[NW][4 * FX_DROW];
   __shared__ __attribute__((aligned(16))) float s_y[NW][2][64];
+  __shared__ __attribute__((aligned(16))) char s_w0[8 * 1024];  // W0/sigma digits (A operand), per chunk
+  __shared__ __attribute__((aligned(16))) float s_hw[NL][20];  // head: W_l (4 x 4) then b_l (4) per layer
   __shared__ float s_hs[NW][NS];
   __shared__ double s_rss[NW];
 
@@ -124,43 +126,35 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
   const BranchDev& bd = st.br[b];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int nch = bd.nchunks;
+  const int nch = NCH ? NCH : bd.nchunks;
   const int64_t n = st.n;
   const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
 
-  // ---- branch constants: head weights (uniform, scalar), W0 digits, column scale ----
+  // ---- branch constants: head weights (LDS, read per tile as broadcasts), W0 digits, column scale ----
   const float* th = st.theta + bd.p_off;
-  float Wh[NL][4][4];  // Wh[l][j][k] = W_l[j][k] (l >= 1), zero padded to 4 x 4
-  float Bh[NH][4];     // Bh[0] = c0 (folded standardisation), Bh[l] = b_l
-#pragma unroll
-  for (int l = 1; l < NL; ++l)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float v = 0.f;
-        if (j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
-        Wh[l][j][k] = ufl(v);
-      }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    Bh[0][k] = ufl(k < bd.widths[0] ? st.fc[b].c0[k] : 0.f);
-#pragma unroll
-    for (int l = 1; l < NH; ++l) Bh[l][k] = ufl(k < bd.widths[l] ? th[bd.boff[l] + k] : 0.f);
+  for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (r < 16) {  // Wh[l][j][k] = W_l[j][k] (l >= 1), zero padded to 4 x 4
+      const int j = r >> 2, k = r & 3;
+      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+    } else {  // bias[0] = c0 (folded standardisation), bias[l] = b_l
+      const int k = r - 16;
+      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+    }
+    s_hw[l][r] = v;
   }
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
   float zscale = st.fc[b].scale[g];
-  v4i adig[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c)
-    adig[c] = c < nch ? *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16)
-                      : v4i{0, 0, 0, 0};
+  for (int c = wave; c < nch; c += NW)  // W0 digit image -> LDS (shared by the four waves)
+    *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
+        *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
   // retire the prologue loads and hide their provenance: inside the tile loop the
   // only vector-memory waits are the explicit, counted ones on this wave's DMAs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(adig[c]));
   asm volatile("" : "+v"(zscale));
+  __syncthreads();
 
   // ---- per-lane LDS offsets ----
   const int gsw = g & 1;
@@ -179,6 +173,9 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
   const int64_t tile_bytes = (int64_t)nch * 1024;
 
   auto issue = [&](int tt, int sl) {
+#if BANN_ABLATE & 8
+    return;  // profiling build: no genotype / target traffic
+#endif
     const char* src = xsrc + (int64_t)tt * tile_bytes;
     char* dst = &s_x[wave][sl][0];
 #pragma unroll
@@ -212,30 +209,57 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
   for (; tt < te; tt += NW, sl ^= 1) {
     const bool more = tt + NW < te;
     if (more) issue(tt + NW, sl ^ 1);
-    vm_wait(more ? nch + 1 : 0);
+    if (NCH != 0) {  // compile-time count: the NCH genotype pieces + the target piece of tile tt + NW
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCH + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      vm_wait(more ? nch + 1 : 0);
+    }
     const char* xs = &s_x[wave][sl][0];
 
     // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
+    // (software pipelined: the LDS reads of chunk c + 1 fly while chunk c's
+    // four MFMAs issue; sched barriers keep the compiler from hoisting more)
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+    {
+      v4u Xc = (v4u)lds_tr8_pair(xs + fo0, xs + fo1);
+      v4i Ac = *reinterpret_cast<const v4i*>(&s_w0[lane * 16]);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      if (c < nch) {
-        const v4u X = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const v4i Bq = (v4i)((X >> (2u * q)) & 0x03030303u);
-#if BANN_ABLATE & 4
-          facc[q] += Bq;
-#else
-          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(adig[c], Bq, facc[q], 0, 0, 0);
-#endif
+      for (int c = 0; c < 8; ++c) {
+        if (NCH == 0 && c >= nch) continue;
+        v4u Xn = Xc;
+        v4i An = Ac;
+        if (c + 1 < 8 && (NCH != 0 || c + 1 < nch)) {
+          Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
+          An = *reinterpret_cast<const v4i*>(&s_w0[(c + 1) * 1024 + lane * 16]);
         }
+        // fragment q = field q of every byte, kept in place (x 4^q, folded into the
+        // digit combine below) except q = 3 (bits 6-7 would overflow int8)
+        const v4i B0 = (v4i)(Xc & 0x03030303u);
+        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
+        const v4i B2 = (v4i)(Xc & 0x30303030u);
+        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
+#if BANN_ABLATE & 4
+        facc[0] += B0 ^ Ac;
+        facc[1] += B1 ^ Ac;
+        facc[2] += B2 ^ Ac;
+        facc[3] += B3 ^ Ac;
+#else
+        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B0, facc[0], 0, 0, 0);
+        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B1, facc[1], 0, 0, 0);
+        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B2, facc[2], 0, 0, 0);
+        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        Xc = Xn;
+        Ac = An;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
-    float z0 = zscale * comb4(facc[0]), z1 = zscale * comb4(facc[1]);
-    float z2 = zscale * comb4(facc[2]), z3 = zscale * comb4(facc[3]);
+    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
     swap32(z0, z2);
     swap32(z1, z3);
     swap16(z0, z1);
@@ -246,7 +270,32 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
     const bool valid = row < n;
     const float yv = s_y[wave][sl][lane];
     float d[4];
+#if BANN_ABLATE & 1
+    d[0] = z0 * 1e-3f - yv;
+    d[1] = z1 * 1e-3f;
+    d[2] = z2 * 1e-3f;
+    d[3] = z3 * 1e-3f;
+    (void)valid;
+    if (false)
+#endif
     {
+      float Wh[NL][4][4], Bh[NH][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l][4 * j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Wh[l][j][k] = r4[k];
+          }
+        }
+        if (l < NH) {
+          const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l][16]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
+        }
+      }
       float z[NH][4], a[NH][4];
       z[0][0] = z0 + Bh[0][0];
       z[0][1] = z1 + Bh[0][1];
@@ -303,6 +352,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
       }
     }
 
+    __builtin_amdgcn_sched_barrier(0);
     // ---- delta0 -> signed digits at the running per-column scale 2^(R - 132) ----
     const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
     const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
@@ -321,26 +371,31 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
       }
     }
     if (grow) {  // rare: rescale the digit sums of the grown columns exactly
-      int rem = g == 0 ? dl[0] : g == 1 ? dl[1] : g == 2 ? dl[2] : dl[3];
-      while (__builtin_amdgcn_ballot_w64(rem > 0) != 0) {
-        const int sh = rem < 7 ? rem : 7;
+      const int sh = g == 0 ? dl[0] : g == 1 ? dl[1] : g == 2 ? dl[2] : dl[3];
 #pragma unroll
-        for (int u = 0; u < 32; ++u)
-          if (u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
-        rem -= sh;
-      }
+      for (int u = 0; u < 32; ++u)
+        if (NCH != 0 || u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
     }
     v4u w;
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - (R[k] ? R[k] : 255));
     *reinterpret_cast<v4u*>(sd_w) = w;
 
-    // ---- backward: dW0 digit sums += G^T delta0 ----
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
+    {
+      constexpr int PD = 8;
+      uint32_t wq[PD];
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      if (u < 4 * nch) {
-        const uint32_t wv = *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe));
+      for (int u = 0; u < PD; ++u)
+        wq[u] = (NCH != 0 || u < 4 * nch) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        if (NCH == 0 && u >= 4 * nch) continue;
+        const uint32_t wv = wq[u % PD];
+        if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
         const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u),
                            (int)((wv >> 4) & 0x03030303u), (int)((wv >> 6) & 0x03030303u)};
 #if BANN_ABLATE & 2
@@ -348,6 +403,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
 #else
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
 #endif
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -430,25 +486,29 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
     st.rss_part[(int64_t)b * st.max_splits + it.split] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
 }
 
-template <int NL>
+template <int NL, int NCH>
 static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
   switch (act) {
-    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0>), grid, block, 0, s, st, items, wp); break;
-    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1>), grid, block, 0, s, st, items, wp); break;
-    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2>), grid, block, 0, s, st, items, wp); break;
-    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3>), grid, block, 0, s, st, items, wp); break;
-    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4>), grid, block, 0, s, st, items, wp); break;
+    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp); break;
+    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp); break;
   }
 }
 
+// full8: every branch of this launch group has exactly 8 chunks
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int write_pred, hipStream_t s) {
+                          int full8, int write_pred, hipStream_t s) {
   if (nitems <= 0) return;
-  switch (L) {
-    case 2: launch_fx_nl<2>(st, items, nitems, act, write_pred, s); break;
-    case 3: launch_fx_nl<3>(st, items, nitems, act, write_pred, s); break;
-    case 4: launch_fx_nl<4>(st, items, nitems, act, write_pred, s); break;
+  switch (L * 2 + (full8 ? 1 : 0)) {
+    case 4: launch_fx_nl<2, 0>(st, items, nitems, act, write_pred, s); break;
+    case 5: launch_fx_nl<2, 8>(st, items, nitems, act, write_pred, s); break;
+    case 6: launch_fx_nl<3, 0>(st, items, nitems, act, write_pred, s); break;
+    case 7: launch_fx_nl<3, 8>(st, items, nitems, act, write_pred, s); break;
+    case 8: launch_fx_nl<4, 0>(st, items, nitems, act, write_pred, s); break;
+    case 9: launch_fx_nl<4, 8>(st, items, nitems, act, write_pred, s); break;
     default: break;
   }
 }

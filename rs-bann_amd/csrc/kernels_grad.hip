@@ -1558,10 +1558,10 @@ static void launch_fused_nl(const DevState& st, const GradItem* items, int32_t n
 }
 
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
-                       int32_t act, int write_pred, hipStream_t s) {
+                       int32_t act, int full8, int write_pred, hipStream_t s) {
   if (nitems <= 0) return;
   if (fused_variant() == 5 && st.u2 && nwaves <= 8) {
-    launch_fused_grad_fx(st, items, nitems, L, act, write_pred, s);
+    launch_fused_grad_fx(st, items, nitems, L, act, full8, write_pred, s);
     return;
   }
   switch (L) {
