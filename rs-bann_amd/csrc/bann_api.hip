@@ -84,6 +84,7 @@ struct bann_ctx {
   int32_t* d_list_scr = nullptr;
   int32_t* d_gen_scr = nullptr;
   GradItem* d_items_scr = nullptr;
+  unsigned long long* d_dbg = nullptr;  // BANN_STAMPS diagnostics
   int64_t items_cap = 0;
   // leapfrog session
   Plan lf;
@@ -151,6 +152,7 @@ static void refresh_state(bann_ctx* ctx) {
   s.pred = ctx->d_pred;
   s.pred0 = ctx->d_pred0;
   s.scr = ctx->d_scr;
+  s.dbg = ctx->d_dbg;
   s.eprec = ctx->d_eprec;
   s.h0 = ctx->d_h0;
   s.htrace = ctx->d_htrace;
@@ -354,6 +356,14 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
   if (!ctx) return BANN_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_dbg) {  // diagnostic build: per-phase cycle sums of the fused kernel
+    unsigned long long h[16] = {};
+    (void)hipMemcpy(h, ctx->d_dbg, sizeof(h), hipMemcpyDeviceToHost);
+    fprintf(stderr, "BANN_STAMPS tiles=%llu cycles/tile:", h[15]);
+    for (int i = 0; i < 8; ++i) fprintf(stderr, " p%d=%.0f", i, h[15] ? (double)h[i] / (double)h[15] : 0.0);
+    fprintf(stderr, "\n");
+    (void)hipFree(ctx->d_dbg);
+  }
   free_plan(ctx->lf);
   void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_xu2, ctx->d_dig, ctx->d_fc, ctx->d_mub,
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
@@ -711,6 +721,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_br, nb));
   CK(hipMemcpyAsync(ctx->d_br, descs.data(), nb * sizeof(BranchDev), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_eprec, eprec.data(), nb * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  if (getenv("BANN_STAMPS")) {
+    CK(hipMalloc((void**)&ctx->d_dbg, 16 * sizeof(unsigned long long)));
+    CK(hipMemsetAsync(ctx->d_dbg, 0, 16 * sizeof(unsigned long long), ctx->stream));
+  }
   ctx->finalized = true;
   int rc = ensure_htrace(ctx, 1);
   if (rc) return rc;

@@ -90,6 +90,7 @@ struct DevState {
   int32_t lint;           // trajectory length L (for the trace stride)
   float max_dh;
   int32_t u2;             // fused branches read xu2 (2-bit) instead of xpk
+  unsigned long long* dbg;  // diagnostic phase stamps (BANN_STAMPS=1 with a BANN_ABLATE=16 build), else null
 };
 
 // ---- launchers (defined in the kernel translation units) ----

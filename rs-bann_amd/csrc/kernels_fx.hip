@@ -107,6 +107,19 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 
 // NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
 // so the LDS reads of a whole phase issue back to back); 0 = any count <= 8.
+#if BANN_ABLATE & 16
+#define FX_STAMP(i)                                   \
+  do {                                                \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_last;                             \
+    t_last = t_;                                      \
+  } while (0)
+#else
+#define FX_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 template <int NL, int ACT, int NCH>
 __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred) {
@@ -172,15 +185,30 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
 
-  auto issue = [&](int tt, int sl) {
+  // LDS-DMA of the NEXT tile is spread over the current tile's forward phase
+  // (one 1 KiB piece per chunk, the target piece in the head): issued in one
+  // burst the pieces back-pressure the wave for thousands of cycles.
+  auto issue_chunk = [&](int tt, int sl, int c) {
 #if BANN_ABLATE & 8
     return;  // profiling build: no genotype / target traffic
 #endif
-    const char* src = xsrc + (int64_t)tt * tile_bytes;
-    char* dst = &s_x[wave][sl][0];
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      if (c < nch) glds16(src + c * 1024, dst + c * 1024);
+    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
+  };
+  // L2 / Infinity-Cache prefetch of a tile two ahead: one dword of each of its
+  // 128-B lines (a single wave instruction for an 8 KiB tile), so the LDS-DMA
+  // that fetches it during the next tile's forward hits on-die
+  const char* const xpf = reinterpret_cast<const char*>(st.xu2) + bd.x_off + (int64_t)min(lane, 8 * nch - 1) * 128;
+  uint32_t pfd = 0;  // destination of the prefetch loads: loop-carried so its register stays reserved
+  auto prefetch_l2 = [&](int tt) {
+#if BANN_ABLATE & 8
+    return;
+#endif
+    asm volatile("global_load_dword %0, %1, off" : "+v"(pfd) : "v"(xpf + (int64_t)tt * tile_bytes) : "memory");
+  };
+  auto issue_y = [&](int tt, int sl) {
+#if BANN_ABLATE & 8
+    return;
+#endif
     const int64_t row = 64 * (int64_t)tt + iota;
     glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
   };
@@ -204,18 +232,34 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
   }
 
+#if BANN_ABLATE & 16
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime(), ntl = 0;
+#endif
   int tt = tb + wave, sl = 0;
-  if (tt < te) issue(tt, 0);
+  bool pf_out = false;  // a prefetch is the youngest outstanding vector-memory op
+  if (tt < te) {
+    if (tt + NW < te) prefetch_l2(tt + NW);
+    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
+    issue_y(tt, 0);
+  }
   for (; tt < te; tt += NW, sl ^= 1) {
     const bool more = tt + NW < te;
-    if (more) issue(tt + NW, sl ^ 1);
-    if (NCH != 0) {  // compile-time count: the NCH genotype pieces + the target piece of tile tt + NW
-      if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NCH + 1) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      vm_wait(more ? nch + 1 : 0);
-    }
+    FX_STAMP(0);
+    // tile tt (issued during tile tt - NW) has landed; the prefetch of tile tt + NW may fly
+    if (pf_out) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FX_STAMP(1);
     const char* xs = &s_x[wave][sl][0];
+#if BANN_ABLATE & 32
+    if (more) {
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, sl ^ 1, c);
+      issue_y(tt + NW, sl ^ 1);
+    }
+    acc[0][0] += xs[lane];
+    pf_out = tt + 2 * NW < te;
+    if (pf_out) prefetch_l2(tt + 2 * NW);
+    continue;
+#endif
 
     // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
     // (software pipelined: the LDS reads of chunk c + 1 fly while chunk c's
@@ -233,6 +277,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
           An = *reinterpret_cast<const v4i*>(&s_w0[(c + 1) * 1024 + lane * 16]);
         }
+        if (more) issue_chunk(tt + NW, sl ^ 1, c);
         // fragment q = field q of every byte, kept in place (x 4^q, folded into the
         // digit combine below) except q = 3 (bits 6-7 would overflow int8)
         const v4i B0 = (v4i)(Xc & 0x03030303u);
@@ -256,6 +301,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(2);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
@@ -269,6 +315,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     const int64_t row = 64 * (int64_t)tt + iota;
     const bool valid = row < n;
     const float yv = s_y[wave][sl][lane];
+    if (more) issue_y(tt + NW, sl ^ 1);
     float d[4];
 #if BANN_ABLATE & 1
     d[0] = z0 * 1e-3f - yv;
@@ -353,21 +400,34 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     }
 
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(3);
     // ---- delta0 -> signed digits at the running per-column scale 2^(R - 132) ----
-    const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
-    const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
-    const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
-    int dl[4];
+    // running scale check: a column needs a (new) scale only when some lane's
+    // |delta| reaches 2^(R - 126) (or R is unset); then the exact wave max of
+    // the exponent fields sets it (rare after the first tile)
+    int dl[4] = {0, 0, 0, 0};
     bool grow = false;
+    {
+      bool need = false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      dl[k] = 0;
-      if (E[k] >= 6 && (R[k] == 0 || E[k] > R[k])) {  // first scale, or |delta| outgrew it
-        if (R[k] != 0) {
-          dl[k] = E[k] + 2 - R[k];
-          grow = true;
+      for (int k = 0; k < 4; ++k) {
+        const int ek = (int)((fbits(d[k]) >> 23) & 0xFFu);
+        need = need || __builtin_amdgcn_ballot_w64(ek > (R[k] ? R[k] : 5)) != 0;
+      }
+      if (need) {
+        const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+        const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+        const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (E[k] >= 6 && (R[k] == 0 || E[k] > R[k])) {  // first scale, or |delta| outgrew it
+            if (R[k] != 0) {
+              dl[k] = E[k] + 2 - R[k];
+              grow = true;
+            }
+            R[k] = E[k] + 2;
+          }
         }
-        R[k] = E[k] + 2;
       }
     }
     if (grow) {  // rare: rescale the digit sums of the grown columns exactly
@@ -382,6 +442,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     *reinterpret_cast<v4u*>(sd_w) = w;
 
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(4);
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
@@ -406,8 +467,20 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    FX_STAMP(5);
+#if BANN_ABLATE & 16
+    ++ntl;
+#endif
+    pf_out = tt + 2 * NW < te;
+    if (pf_out) prefetch_l2(tt + 2 * NW);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if BANN_ABLATE & 16
+  if (lane == 0 && st.dbg) {
+    for (int i = 0; i < 6; ++i) atomicAdd(&st.dbg[i], ph[i]);
+    atomicAdd(&st.dbg[15], ntl);
+  }
+#endif
 
   // ---- workgroup reduction (fixed order: deterministic) ----
   {
