@@ -1,0 +1,124 @@
+/*
+ * bann_net.h — C ABI of the sequential network driver: Net<B>::train over the
+ * HIP branch kernels of bann.h, and the Net<B> model file.
+ *
+ * Replaces (medical-genomics-group/rs-bann):
+ *   Net::train             src/net/net.rs:201-358 (HMC path: per sweep, branches
+ *                          in shuffled order, each against the residual refreshed
+ *                          after the previous one -- the reference's Gibbs order)
+ *   initialize_stats       src/net/net.rs:158-171
+ *   OutputBias             src/net/net.rs:29-72
+ *   LogPosteriorDensity    src/net/log_posterior_density.rs:18-68
+ *   TrainingStats          src/net/train_stats.rs:24-88
+ *   GlobalParams           src/net/params.rs:13-63
+ *   Net::to_file/from_file src/net/net.rs:107-115 (bincode 1.3 legacy encoding of
+ *                          the Net<B> struct)
+ *
+ * The per-branch math (predict, the HMC trajectory, step sizes) runs on the
+ * device through bann.h; the Gibbs precision draws, the residual bookkeeping
+ * (n floats), the output bias and the log posterior density stay on the host,
+ * as in the reference (north_star: "the Gibbs hyperparameter sweep stays on the
+ * host").  Same conventions as bann.h: int status codes, host pointers read or
+ * written inside the call and never retained.
+ */
+#ifndef BANN_NET_H
+#define BANN_NET_H
+
+#include <stdint.h>
+
+#include "bann.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bann_net bann_net;
+
+/* NetworkPrecisionHyperparameters (params.rs:134-142): Gamma (shape, scale) of
+ * the precision priors of the dense, summary and output layers.  The reference
+ * default is vague: shape 0.001, scale 1000 (params.rs:119-124). */
+typedef struct {
+  float dense_shape, dense_scale;
+  float summary_shape, summary_scale;
+  float output_shape, output_scale;
+} bann_precision_hyperparams;
+
+/* The MCMCCfg fields (mcmc_cfg.rs:181-204) Net::train reads on its HMC path.
+ * Defaults (MCMCCfgBuilder::default, mcmc_cfg.rs:34-56): factor 1, max error 10,
+ * L 100, Izmailov, chain 100, burn_in chain-1, precisions sampled, ML bias. */
+typedef struct {
+  float hmc_step_size_factor;
+  float hmc_max_hamiltonian_error;
+  int32_t hmc_integration_length;
+  int32_t hmc_step_size_mode; /* bann_step_mode: BANN_STEP_IZMAILOV or BANN_STEP_UNIFORM */
+  int32_t chain_length;
+  int32_t burn_in;
+  int32_t fixed_param_precisions;
+  int32_t sampled_output_bias;
+} bann_mcmc_cfg;
+
+/* Host random source for the driver's draws (the reference's ThreadRng,
+ * net.rs:218 and branch rng_mut()).  A NULL member selects the built-in
+ * generator (mt19937_64 seeded at bann_net_create).  Tests install hooks that
+ * replay the oracle's stream.  Draw order per branch update: error precision
+ * (1 gamma); unless fixed precisions, per layer l < L-1 the weight precisions
+ * (one gamma per input node for ARD priors, else one) then the bias precision
+ * (1 gamma), then the output-layer precision (1 gamma); the momentum (P
+ * normals, param_vec order); the acceptance uniform (1 uniform); then, with
+ * sampled output bias, 1 gamma + 1 normal.  Each sweep starts with the branch
+ * shuffle: nb-1 uniforms (Fisher-Yates, i = nb-1 .. 1, j = floor(u (i+1))). */
+typedef struct {
+  void* user;
+  double (*uniform)(void* user);
+  double (*normal)(void* user);
+  double (*gamma)(void* user, double shape, double scale);
+} bann_rng_hooks;
+
+/* Summary of TrainingStats + the current global state. */
+typedef struct {
+  uint64_t num_samples, num_accepted, num_early_rejected;
+  int32_t num_records;    /* entries of mse_train / lpd recorded so far */
+  float mse_train_last;   /* sum(residual^2) / n at the last record (net.rs:597-610) */
+  float lpd_last;         /* LogPosteriorDensity::lpd at the last record */
+  float output_bias;      /* OutputBias::bias */
+  float error_precision;  /* GlobalParams::error_precision */
+  float output_layer_precision;
+  float output_reg_sum;   /* GlobalParams::output_weight_summary_stats.reg_sum */
+} bann_train_summary;
+
+/* A network over every branch of a finalized context.  Global state follows
+ * BlockNetCfg::build_net (architectures.rs:187-237): error precision 2,
+ * output-layer precision = branch 0's current output precision, the output
+ * weight summary statistic summed over branches (sum of squares for ridge
+ * priors, sum of abs for lasso), OutputBias {2, 1, 0}.  The context's branch
+ * params / precisions are the initial BranchCfgs.  std-normal branches are
+ * rejected with BANN_E_ARG: the reference panics in Net::train for them
+ * (log_posterior_density.rs:55 -> std_normal_branch.rs:129 unimplemented!). */
+int bann_net_create(bann_ctx* ctx, const bann_precision_hyperparams* hp, uint64_t seed, bann_net** out);
+int bann_net_destroy(bann_net* net);
+int bann_net_set_rng_hooks(bann_net* net, const bann_rng_hooks* hooks);
+/* override GlobalParams / OutputBias (e.g. to continue a loaded chain) */
+int bann_net_set_global(bann_net* net, float error_precision, float output_layer_precision, float output_bias,
+                        float output_bias_precision);
+/* Net::train (net.rs:201-358) on the phenotype y[n].  outdir (may be NULL):
+ * models/<chain_ix>.bin after burn-in (net.rs:338-342, 565-569) and
+ * training_stats (JSON, train_stats.rs:83-87). */
+int bann_net_train(bann_net* net, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir);
+int bann_net_summary(const bann_net* net, bann_train_summary* out);
+/* the recorded mse_train / lpd series (TrainingStats::mse_train / lpd);
+ * writes min(cap, num_records) entries of each (either may be NULL) */
+int bann_net_records(const bann_net* net, float* mse_train, float* lpd, int32_t cap);
+/* the residual y - bias - sum_b f_b after the last branch update (n floats) */
+int bann_net_residual(const bann_net* net, float* out);
+/* Net::to_file (net.rs:112-115): bincode Net<B> of the current state */
+int bann_net_save(const bann_net* net, const char* path);
+/* Net::from_file (net.rs:107-110): read a bincode Net<B> whose branches match
+ * the context's (count, markers, layer widths); loads params / precisions into
+ * the context and the global state, output bias, stats and LPD into the net. */
+int bann_net_load(bann_net* net, const char* path);
+const char* bann_net_last_error(const bann_net* net);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BANN_NET_H */

@@ -572,7 +572,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     d.fused = ok ? 1 : 0;
     if (d.fused) total_frags += ctx->nfrag;
   }
-  int64_t target_items = 8192;
+  int64_t target_items = 1024;  // fewer, longer items: -1..2 % (prologue + barrier skew)
   if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
   int64_t min_frags = 64;  // >= 16 tiles per work item amortises the per-item prologue/epilogue
   if (const char* e = getenv("BANN_MIN_FRAGS")) min_frags = std::max<int64_t>(1, atoll(e));
