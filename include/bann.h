@@ -107,6 +107,12 @@ int bann_finalize(bann_ctx* ctx, int32_t free_raw);
 int bann_num_branches(const bann_ctx* ctx);
 int64_t bann_num_params(const bann_ctx* ctx, int32_t b);
 int64_t bann_num_precisions(const bann_ctx* ctx, int32_t b);
+/* shape of branch b (the BranchCfg header fields, branch_cfg.rs:8-16):
+ * markers, number of layers, layer widths (min(num_layers, widths_cap)
+ * entries), activation (bann_activation) and prior (bann_prior); any output
+ * may be NULL.  Callable before finalize and without compute. */
+int bann_branch_info(const bann_ctx* ctx, int32_t b, int32_t* m, int32_t* num_layers, int32_t* widths_out,
+                     int32_t widths_cap, int32_t* activation, int32_t* prior);
 
 /* BranchParams::from_host / load_param_vec (params.rs:634-698) */
 int bann_branch_set_params(bann_ctx* ctx, int32_t b, const float* param_vec);
@@ -193,11 +199,18 @@ int bann_synchronize(bann_ctx* ctx);
 int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms);
 
 /* ---------------- introspection for tests / profiling ---------------- */
-/* which gradient kernel serves branch b: 1 = fused single-pass MFMA/VALU kernel,
- * 0 = generic multi-pass kernels */
+/* which gradient kernel serves branch b: 1 = fused single-pass kernel (every
+ * width <= 4), 2 = wide fused kernel (one hidden layer, W, S <= 32, m <= 128:
+ * masked layer on i8 MFMA, hidden GEMMs on f32 or bf16 MFMA), 0 = generic
+ * multi-pass kernels */
 int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
 /* name of the fused gradient kernel family used for branches of <= 512 markers */
 const char* bann_fused_kernel_name(void);
+/* wide kernel: run the hidden-layer GEMMs (forward, error propagation, dW1) on
+ * bf16 MFMA (1) instead of exact f32 MFMA (0, default).  BASELINE config C5's
+ * "bf16 hidden GEMM on MFMA vs fp32": 16x the matrix rate, bf16 operand
+ * rounding (~1e-3 relative on gradients; not parity-exact).  Any time. */
+int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled);
 /* force every branch onto the generic path (0) or allow the fused path (1) */
 int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
 /* bytes of packed genotype data read per full gradient evaluation of all branches */

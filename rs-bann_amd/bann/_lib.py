@@ -13,6 +13,7 @@ PKG_ROOT = os.path.dirname(HERE)                       # rs-bann_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 LIB_PATH = os.environ.get("BANN_LIB", os.path.join(PKG_ROOT, "librsbann_amd.so"))
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "bann.h")
+HEADER_PATHS = [HEADER_PATH, os.path.join(REPO_ROOT, "include", "bann_net.h")]
 
 BANN_OK = 0
 STATUS = {0: "BANN_OK", -1: "BANN_E_HIP", -2: "BANN_E_SHAPE", -3: "BANN_E_OOM", -4: "BANN_E_STATE",
@@ -38,7 +39,41 @@ _i32, _i64, _u64, _f32, _f64 = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_
 _pi8, _pu8 = C.POINTER(C.c_int8), C.POINTER(C.c_uint8)
 _pi32, _pf32, _pf64 = C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(C.c_double)
 
-# name -> (restype, argtypes); mirrors include/bann.h one to one
+
+
+class PrecisionHyperparams(C.Structure):
+    """bann_precision_hyperparams (NetworkPrecisionHyperparameters, params.rs:134-142)"""
+    _fields_ = [("dense_shape", C.c_float), ("dense_scale", C.c_float), ("summary_shape", C.c_float),
+                ("summary_scale", C.c_float), ("output_shape", C.c_float), ("output_scale", C.c_float)]
+
+
+class McmcCfg(C.Structure):
+    """bann_mcmc_cfg (the MCMCCfg fields of Net::train's HMC path, mcmc_cfg.rs:181-204)"""
+    _fields_ = [("hmc_step_size_factor", C.c_float), ("hmc_max_hamiltonian_error", C.c_float),
+                ("hmc_integration_length", C.c_int32), ("hmc_step_size_mode", C.c_int32),
+                ("chain_length", C.c_int32), ("burn_in", C.c_int32), ("fixed_param_precisions", C.c_int32),
+                ("sampled_output_bias", C.c_int32)]
+
+
+UNIFORM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
+NORMAL_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
+GAMMA_FN = C.CFUNCTYPE(C.c_double, C.c_void_p, C.c_double, C.c_double)
+
+
+class RngHooks(C.Structure):
+    """bann_rng_hooks: host random source of the network driver"""
+    _fields_ = [("user", C.c_void_p), ("uniform", UNIFORM_FN), ("normal", NORMAL_FN), ("gamma", GAMMA_FN)]
+
+
+class TrainSummary(C.Structure):
+    """bann_train_summary (TrainingStats + global state)"""
+    _fields_ = [("num_samples", C.c_uint64), ("num_accepted", C.c_uint64), ("num_early_rejected", C.c_uint64),
+                ("num_records", C.c_int32), ("mse_train_last", C.c_float), ("lpd_last", C.c_float),
+                ("output_bias", C.c_float), ("error_precision", C.c_float), ("output_layer_precision", C.c_float),
+                ("output_reg_sum", C.c_float)]
+
+
+# name -> (restype, argtypes); mirrors include/bann.h and include/bann_net.h one to one
 SIGNATURES = {
     "bann_ctx_create": (C.c_int, [C.c_int, C.POINTER(_P)]),
     "bann_ctx_destroy": (C.c_int, [_P]),
@@ -55,6 +90,7 @@ SIGNATURES = {
     "bann_num_branches": (C.c_int, [_P]),
     "bann_num_params": (_i64, [_P, _i32]),
     "bann_num_precisions": (_i64, [_P, _i32]),
+    "bann_branch_info": (C.c_int, [_P, _i32, _pi32, _pi32, _pi32, _i32, _pi32, _pi32]),
     "bann_branch_set_params": (C.c_int, [_P, _i32, _pf32]),
     "bann_branch_get_params": (C.c_int, [_P, _i32, _pf32]),
     "bann_branch_set_precisions": (C.c_int, [_P, _i32, _pf32]),
@@ -81,7 +117,20 @@ SIGNATURES = {
     "bann_profile_session": (C.c_int, [_P, _i32, _pf32, _pf32]),
     "bann_branch_kernel_path": (C.c_int, [_P, _i32]),
     "bann_set_fused_enabled": (C.c_int, [_P, _i32]),
+    "bann_set_hidden_gemm_bf16": (C.c_int, [_P, _i32]),
     "bann_packed_genotype_bytes": (_i64, [_P]),
+    # bann_net.h: the Net::train driver and the Net<B> model file
+    "bann_net_create": (C.c_int, [_P, C.POINTER(PrecisionHyperparams), _u64, C.POINTER(_P)]),
+    "bann_net_destroy": (C.c_int, [_P]),
+    "bann_net_set_rng_hooks": (C.c_int, [_P, C.POINTER(RngHooks)]),
+    "bann_net_set_global": (C.c_int, [_P, _f32, _f32, _f32, _f32]),
+    "bann_net_train": (C.c_int, [_P, _pf32, _i64, C.POINTER(McmcCfg), C.c_char_p]),
+    "bann_net_summary": (C.c_int, [_P, C.POINTER(TrainSummary)]),
+    "bann_net_records": (C.c_int, [_P, _pf32, _pf32, _i32]),
+    "bann_net_residual": (C.c_int, [_P, _pf32]),
+    "bann_net_save": (C.c_int, [_P, C.c_char_p]),
+    "bann_net_load": (C.c_int, [_P, C.c_char_p]),
+    "bann_net_last_error": (C.c_char_p, [_P]),
 }
 
 _lib = None

@@ -120,7 +120,12 @@ class BannContext:
         return int(self._check(self._lib.bann_num_precisions(self._h, b)))
 
     def kernel_path(self, b: int) -> str:
-        return "fused" if self._check(self._lib.bann_branch_kernel_path(self._h, b)) == 1 else "generic"
+        """"fused" (widths <= 4), "wide" (one hidden layer <= 32 x 32) or "generic"."""
+        return {1: "fused", 2: "wide"}.get(self._check(self._lib.bann_branch_kernel_path(self._h, b)), "generic")
+
+    def set_hidden_gemm_bf16(self, enabled: bool):
+        """wide kernel: hidden GEMMs on bf16 MFMA (reduced precision) instead of f32 MFMA."""
+        self._check(self._lib.bann_set_hidden_gemm_bf16(self._h, 1 if enabled else 0))
 
     def fused_kernel_name(self) -> str:
         return self._lib.bann_fused_kernel_name().decode()

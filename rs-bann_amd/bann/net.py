@@ -1,0 +1,119 @@
+"""Host mirror of include/bann_net.h: the sequential network driver.
+
+``Net`` wraps a ``bann_net`` over a finalized ``BannContext``: ``train`` is
+``Net::train`` (src/net/net.rs:201-358) -- per sweep the branches in shuffled
+order, each fitted by one HMC trajectory on the device against the residual
+refreshed after the previous branch, Gibbs precision draws, the output bias and
+the log posterior density on the host -- and ``save`` / ``load`` are
+``Net::to_file`` / ``from_file`` (net.rs:107-115, bincode ``Net<B>``).  All
+computation is in librsbann_amd.so (C++ driver + HIP kernels).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+
+from ._lib import (GAMMA_FN, NORMAL_FN, STEP_MODES, UNIFORM_FN, BannError, McmcCfg, PrecisionHyperparams,
+                   RngHooks, TrainSummary)
+
+VAGUE = (0.001, 1000.0)  # PrecisionHyperparameters::vague (params.rs:119-124)
+
+
+@dataclass
+class MCMCConfig:
+    """The MCMCCfg fields of Net::train's HMC path; defaults of MCMCCfgBuilder::default
+    (mcmc_cfg.rs:34-56).  burn_in None -> chain_length - 1 (mcmc_cfg.rs:152-156)."""
+    hmc_step_size_factor: float = 1.0
+    hmc_max_hamiltonian_error: float = 10.0
+    hmc_integration_length: int = 100
+    hmc_step_size_mode: str = "izmailov"
+    chain_length: int = 100
+    burn_in: Optional[int] = None
+    fixed_param_precisions: bool = False
+    sampled_output_bias: bool = False
+
+    def to_c(self) -> McmcCfg:
+        burn = self.chain_length - 1 if self.burn_in is None else self.burn_in
+        return McmcCfg(self.hmc_step_size_factor, self.hmc_max_hamiltonian_error, self.hmc_integration_length,
+                       STEP_MODES[self.hmc_step_size_mode], self.chain_length, max(burn, 0),
+                       int(self.fixed_param_precisions), int(self.sampled_output_bias))
+
+
+class Net:
+    """Net<B> over every branch of ``ctx`` (branch params / precisions = the
+    initial BranchCfgs).  hyperparams: ((dense shape, scale), (summary ...),
+    (output ...)) = NetworkPrecisionHyperparameters."""
+
+    def __init__(self, ctx, hyperparams: Tuple = (VAGUE, VAGUE, VAGUE), seed: int = 0):
+        self._ctx = ctx
+        self._lib = ctx._lib
+        (ds, dc), (ss, sc), (os_, oc) = hyperparams
+        self.hyperparams = hyperparams
+        hp = PrecisionHyperparams(ds, dc, ss, sc, os_, oc)
+        h = C.c_void_p()
+        rc = self._lib.bann_net_create(ctx._h, C.byref(hp), seed, C.byref(h))
+        if rc != 0:
+            raise BannError(rc, "bann_net_create failed (std-normal branches cannot be trained, net.rs:167)")
+        self._h = h
+        self._hooks = None
+
+    def _check(self, rc):
+        if rc < 0:
+            raise BannError(rc, self._lib.bann_net_last_error(self._h).decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.bann_net_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_rng(self, uniform: Callable[[], float], normal: Callable[[], float],
+                gamma: Callable[[float, float], float]):
+        """replace the driver's host RNG (draw order: include/bann_net.h)."""
+        self._hooks = RngHooks(None, UNIFORM_FN(lambda _u: uniform()), NORMAL_FN(lambda _u: normal()),
+                               GAMMA_FN(lambda _u, k, s: gamma(k, s)))
+        self._check(self._lib.bann_net_set_rng_hooks(self._h, C.byref(self._hooks)))
+
+    def set_global(self, error_precision: float, output_layer_precision: float, output_bias: float = 0.0,
+                   output_bias_precision: float = 1.0):
+        self._check(self._lib.bann_net_set_global(self._h, error_precision, output_layer_precision, output_bias,
+                                                  output_bias_precision))
+
+    def train(self, y, cfg: MCMCConfig = MCMCConfig(), outdir: Optional[str] = None):
+        v = np.ascontiguousarray(y, dtype=np.float32)
+        self._check(self._lib.bann_net_train(self._h, v.ctypes.data_as(C.POINTER(C.c_float)), v.size,
+                                             C.byref(cfg.to_c()), outdir.encode() if outdir else None))
+
+    def summary(self) -> dict:
+        s = TrainSummary()
+        self._check(self._lib.bann_net_summary(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in TrainSummary._fields_}
+
+    def records(self):
+        """(mse_train, lpd) series of TrainingStats (train_stats.rs:24-32)."""
+        k = self.summary()["num_records"]
+        mse = np.zeros(k, np.float32)
+        lpd = np.zeros(k, np.float32)
+        self._check(self._lib.bann_net_records(self._h, mse.ctypes.data_as(C.POINTER(C.c_float)),
+                                               lpd.ctypes.data_as(C.POINTER(C.c_float)), k))
+        return mse, lpd
+
+    def residual(self) -> np.ndarray:
+        out = np.zeros(self._ctx.n, np.float32)
+        self._check(self._lib.bann_net_residual(self._h, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def save(self, path: str):
+        self._check(self._lib.bann_net_save(self._h, path.encode()))
+
+    def load(self, path: str):
+        self._check(self._lib.bann_net_load(self._h, path.encode()))

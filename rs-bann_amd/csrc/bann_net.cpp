@@ -1,0 +1,740 @@
+// bann_net.cpp — host side of the sequential network driver (include/bann_net.h):
+// Net<B>::train over the HIP branch kernels of bann.h, the Gibbs precision
+// draws, the output bias, the log posterior density, TrainingStats and the
+// bincode Net<B> model file.
+//
+// Host C++ only.  Every per-branch computation (predict, the HMC trajectory with
+// its device step sizes and gradients) goes through the bann.h entry points;
+// what stays here is what the reference also runs on the host between branch
+// updates: n-float residual bookkeeping, Gamma/Normal draws from host RNG,
+// scalar log-density terms (net.rs:201-358).
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/bann_net.h"
+
+namespace {
+
+enum { P_RIDGE_ARD = 0, P_RIDGE_BASE = 1, P_LASSO_ARD = 2, P_LASSO_BASE = 3, P_STD_NORMAL = 4 };
+bool is_ard(int prior) { return prior == P_RIDGE_ARD || prior == P_LASSO_ARD; }
+bool is_lasso(int prior) { return prior == P_LASSO_ARD || prior == P_LASSO_BASE; }
+
+// One branch: the BranchCfg (branch_cfg.rs:8-16) held on the host between
+// updates, with the offsets of its layers in the param / precision vectors.
+struct Branch {
+  int m = 0, L = 0, act = 0, prior = 0;
+  std::vector<int> widths, win;        // out / in width of layer l
+  std::vector<int64_t> woff, boff;     // param_vec offsets of W_l (in x out, col-major) and b_l
+  std::vector<int64_t> wpoff, wpn;     // precision_vec offset / count of layer l's weight precisions
+  int64_t bpoff = 0, epoff = 0;        // first bias precision, the error precision
+  int64_t P = 0, NP = 0, num_weights = 0;
+  std::vector<float> params, prec;     // BranchParamsHost / BranchPrecisionsHost as flat vectors
+  float ows_reg_sum = 0.f;             // BranchParamsHost::output_weight_summary_stats
+  uint64_t ows_num = 0;
+
+  int64_t out_prec_ix() const { return wpoff[L - 1]; }
+  // summary_stat_fn_host of the output weights (ridge_ard.rs:39-41, lasso_ard.rs:45-47)
+  double out_stat() const {
+    const float* w = params.data() + woff[L - 1];
+    double s = 0.0;
+    for (int j = 0; j < win[L - 1]; ++j) s += is_lasso(prior) ? std::fabs((double)w[j]) : (double)w[j] * w[j];
+    return s;
+  }
+};
+
+struct Writer {  // bincode 1.3 legacy config: fixint, little-endian
+  std::vector<uint8_t> b;
+  void raw(const void* p, size_t k) { b.insert(b.end(), (const uint8_t*)p, (const uint8_t*)p + k); }
+  void u8(uint8_t v) { raw(&v, 1); }
+  void u32(uint32_t v) { raw(&v, 4); }
+  void u64(uint64_t v) { raw(&v, 8); }
+  void f32(float v) { raw(&v, 4); }
+  void vf32(const float* p, size_t k) {
+    u64(k);
+    raw(p, 4 * k);
+  }
+  void vu64(const std::vector<int>& v) {
+    u64(v.size());
+    for (int x : v) u64((uint64_t)x);
+  }
+};
+
+struct Reader {
+  const uint8_t* p;
+  size_t n, pos = 0;
+  bool ok = true;
+  void raw(void* d, size_t k) {
+    if (!ok || pos + k > n) {
+      ok = false;
+      std::memset(d, 0, k);
+      return;
+    }
+    std::memcpy(d, p + pos, k);
+    pos += k;
+  }
+  uint8_t u8() {
+    uint8_t v;
+    raw(&v, 1);
+    return v;
+  }
+  uint32_t u32() {
+    uint32_t v;
+    raw(&v, 4);
+    return v;
+  }
+  uint64_t u64() {
+    uint64_t v;
+    raw(&v, 8);
+    return v;
+  }
+  float f32() {
+    float v;
+    raw(&v, 4);
+    return v;
+  }
+  std::vector<float> vf32() {
+    const uint64_t k = u64();
+    if (!ok || k > (n - pos) / 4) {
+      ok = false;
+      return {};
+    }
+    std::vector<float> v(k);
+    raw(v.data(), 4 * k);
+    return v;
+  }
+  std::vector<uint64_t> vu64() {
+    const uint64_t k = u64();
+    if (!ok || k > (n - pos) / 8) {
+      ok = false;
+      return {};
+    }
+    std::vector<uint64_t> v(k);
+    for (auto& x : v) x = u64();
+    return v;
+  }
+};
+
+}  // namespace
+
+struct bann_net {
+  bann_ctx* ctx = nullptr;
+  bann_precision_hyperparams hp{};
+  std::mt19937_64 gen;
+  bann_rng_hooks hooks{};
+  std::string err;
+  std::vector<Branch> br;
+  int64_t n = 0;
+  std::vector<float> residual;
+  // GlobalParams (params.rs:13-18)
+  float g_eprec = 2.f, g_oprec = 0.05f, g_reg_sum = 0.f;
+  uint64_t g_num = 0;
+  // OutputBias (net.rs:29-36); build_net's initial value (architectures.rs:224-228)
+  float ob_eprec = 2.f, ob_prec = 1.f, ob_bias = 0.f;
+  // TrainingStats (train_stats.rs:24-32)
+  uint64_t ns = 0, nacc = 0, nearly = 0;
+  std::vector<float> mse, lpd;
+  // LogPosteriorDensity (log_posterior_density.rs:9-16)
+  float lpd_rss = -INFINITY, lpd_outw = -INFINITY;
+  std::vector<float> lpd_local;
+};
+
+namespace {
+
+int fail(bann_net* t, int code, const std::string& msg) {
+  if (t) t->err = msg;
+  return code;
+}
+#define CKB(call)                                                                                   \
+  do {                                                                                              \
+    const int rc_ = (call);                                                                         \
+    if (rc_ < 0) return fail(t, rc_, std::string(#call) + ": " + bann_last_error(t->ctx));         \
+  } while (0)
+
+double draw_uniform(bann_net* t) {
+  if (t->hooks.uniform) return t->hooks.uniform(t->hooks.user);
+  return std::uniform_real_distribution<double>(0.0, 1.0)(t->gen);
+}
+double draw_normal(bann_net* t) {
+  if (t->hooks.normal) return t->hooks.normal(t->hooks.user);
+  return std::normal_distribution<double>(0.0, 1.0)(t->gen);
+}
+double draw_gamma(bann_net* t, double shape, double scale) {
+  if (t->hooks.gamma) return t->hooks.gamma(t->hooks.user, shape, scale);
+  return std::gamma_distribution<double>(shape, scale)(t->gen);
+}
+
+// NetworkPrecisionHyperparameters::layer_prior_hyperparams (params.rs:146-163)
+void layer_hp(const bann_net* t, int l, int L, double& shape, double& scale) {
+  if (l == L - 1) {
+    shape = t->hp.output_shape;
+    scale = t->hp.output_scale;
+  } else if (l == L - 2) {
+    shape = t->hp.summary_shape;
+    scale = t->hp.summary_scale;
+  } else {
+    shape = t->hp.dense_shape;
+    scale = t->hp.dense_scale;
+  }
+}
+
+// gibbs_steps.rs:76-94 / 113-129 (ridge) and 25-57 (lasso): Gamma posterior draws
+double ridge_posterior(bann_net* t, double shape, double scale, double sum_sq, double num) {
+  return draw_gamma(t, shape + num / 2.0, 2.0 * scale / (2.0 + scale * sum_sq));
+}
+double lasso_posterior(bann_net* t, double shape, double scale, double sum_abs, double num) {
+  return draw_gamma(t, shape + num, scale / (1.0 + scale * sum_abs));
+}
+
+double sum_sq(const float* v, int64_t k) {
+  double s = 0.0;
+  for (int64_t i = 0; i < k; ++i) s += (double)v[i] * v[i];
+  return s;
+}
+double sum_abs(const float* v, int64_t k) {
+  double s = 0.0;
+  for (int64_t i = 0; i < k; ++i) s += std::fabs((double)v[i]);
+  return s;
+}
+
+// BranchCfg::update_global_params (branch_cfg.rs:59-63)
+void cfg_update_global(bann_net* t, Branch& B) {
+  B.prec[B.epoff] = t->g_eprec;
+  B.prec[B.out_prec_ix()] = t->g_oprec;
+  B.ows_reg_sum = t->g_reg_sum;
+  B.ows_num = t->g_num;
+}
+
+// sample_prior_precisions: ridge_ard.rs:271-301, lasso_ard.rs:271-298,
+// ridge_base.rs / lasso_base.rs (whole-layer draws); biases always ridge.
+void sample_prior_precisions(bann_net* t, Branch& B) {
+  for (int l = 0; l < B.L - 1; ++l) {
+    double shape, scale;
+    layer_hp(t, l, B.L, shape, scale);
+    const float* W = B.params.data() + B.woff[l];
+    const int in = B.win[l], out = B.widths[l];
+    if (is_ard(B.prior)) {
+      for (int j = 0; j < in; ++j) {  // one precision per input node (row of W_l)
+        double s = 0.0;
+        for (int k = 0; k < out; ++k) {
+          const double w = W[(int64_t)k * in + j];
+          s += B.prior == P_LASSO_ARD ? std::fabs(w) : w * w;
+        }
+        B.prec[B.wpoff[l] + j] = (float)(B.prior == P_LASSO_ARD ? draw_gamma(t, out + shape, scale / (1.0 + scale * s))
+                                                                : draw_gamma(t, out / 2.0 + shape,
+                                                                             2.0 * scale / (2.0 + scale * s)));
+      }
+    } else if (B.prior == P_LASSO_BASE) {
+      B.prec[B.wpoff[l]] = (float)lasso_posterior(t, shape, scale, sum_abs(W, (int64_t)in * out), (double)in * out);
+    } else {
+      B.prec[B.wpoff[l]] = (float)ridge_posterior(t, shape, scale, sum_sq(W, (int64_t)in * out), (double)in * out);
+    }
+    const float* b = B.params.data() + B.boff[l];
+    B.prec[B.bpoff + l] = (float)ridge_posterior(t, shape, scale, sum_sq(b, out), out);
+  }
+}
+
+// log_density_joint_wrt_biases (branch_sampler.rs:260-279) + _wrt_local_weights
+// (ridge_ard.rs:119-148, ridge_base.rs:119-137, lasso_ard.rs:119-149, lasso_base.rs:119-137)
+double ld_joint_local(const bann_net* t, const Branch& B) {
+  double ld = 0.0;
+  for (int l = 0; l < B.L - 1; ++l) {
+    double shape, scale;
+    layer_hp(t, l, B.L, shape, scale);
+    const float* b = B.params.data() + B.boff[l];
+    const double lb = B.prec[B.bpoff + l];
+    ld -= lb * (sum_sq(b, B.widths[l]) / 2.0 + 1.0 / scale);
+    ld += (shape + (B.widths[l] - 2.0) / 2.0) * std::log(lb);
+    const float* W = B.params.data() + B.woff[l];
+    const int in = B.win[l], out = B.widths[l];
+    if (is_ard(B.prior)) {
+      for (int j = 0; j < in; ++j) {
+        const double lam = B.prec[B.wpoff[l] + j];
+        double s = 0.0;
+        for (int k = 0; k < out; ++k) {
+          const double w = W[(int64_t)k * in + j];
+          s += B.prior == P_LASSO_ARD ? std::fabs(w) : w * w;
+        }
+        if (B.prior == P_RIDGE_ARD) {
+          ld -= (s / 2.0 + 1.0 / scale) * lam;
+          ld += (shape + (out - 2.0) / 2.0) * std::log(lam);
+        } else {
+          ld -= (s + 1.0 / scale) * lam;
+          ld += (shape + out - 1.0) * std::log(lam);
+        }
+      }
+    } else {
+      const double lam = B.prec[B.wpoff[l]];
+      const double k = (double)in * out;
+      if (B.prior == P_RIDGE_BASE) {
+        ld -= (sum_sq(W, (int64_t)k) / 2.0 + 1.0 / scale) * lam;
+        ld += (shape + (k - 2.0) / 2.0) * std::log(lam);
+      } else {
+        ld -= (sum_abs(W, (int64_t)k) + 1.0 / scale) * lam;
+        ld += (shape + k - 1.0) * std::log(lam);
+      }
+    }
+  }
+  return ld;
+}
+
+// log_density_joint_wrt_output_weights (ridge_ard.rs:150-169, lasso_ard.rs:153-172;
+// base priors identical): global statistic = own + the other branches' (`others`)
+double ld_joint_out(const bann_net* t, const Branch& B, double others) {
+  double shape, scale;
+  layer_hp(t, B.L - 1, B.L, shape, scale);
+  const double lam = B.prec[B.out_prec_ix()];
+  const double num = (double)B.ows_num;
+  if (is_lasso(B.prior)) return -((B.out_stat() + others) + 1.0 / scale) * lam + (shape + num - 1.0) * std::log(lam);
+  return -(0.5 * (B.out_stat() + others) + 1.0 / scale) * lam + (shape + (num - 2.0) / 2.0) * std::log(lam);
+}
+
+// LogPosteriorDensity::update_from_branch (log_posterior_density.rs:27-61)
+void update_lpd(bann_net* t, int b, double others) {
+  const Branch& B = t->br[b];
+  t->lpd_local[b] = (float)ld_joint_local(t, B);
+  t->lpd_outw = (float)ld_joint_out(t, B, others);
+  const double rss = sum_sq(t->residual.data(), t->n);
+  const double le = B.prec[B.epoff];
+  t->lpd_rss = (float)(std::log(le) * (t->hp.output_shape + (t->n - 2.0) / 2.0) -
+                       le * (rss / 2.0 + 1.0 / t->hp.output_scale));
+}
+
+// Net::record_perf (net.rs:597-610), without test data
+void record_perf(bann_net* t) {
+  double l = (double)t->lpd_rss + t->lpd_outw;
+  for (float v : t->lpd_local) l += v;
+  t->lpd.push_back((float)l);
+  t->mse.push_back((float)(sum_sq(t->residual.data(), t->n) / (double)t->n));
+}
+
+bool mkdir_p(const std::string& d) {
+  if (d.empty()) return true;
+  std::string cur;
+  for (size_t i = 0; i < d.size(); ++i) {
+    cur += d[i];
+    if ((d[i] == '/' || i + 1 == d.size()) && cur != "/") {
+      if (mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+  }
+  return true;
+}
+
+Writer serialize(const bann_net* t) {
+  Writer w;
+  const auto& hp = t->hp;  // NetworkPrecisionHyperparameters (params.rs:134-142)
+  w.f32(hp.dense_shape);
+  w.f32(hp.dense_scale);
+  w.f32(hp.summary_shape);
+  w.f32(hp.summary_scale);
+  w.f32(hp.output_shape);
+  w.f32(hp.output_scale);
+  w.u64(t->br.size());  // num_branches
+  w.u64(t->br.size());  // branch_cfgs: Vec<BranchCfg>
+  for (const Branch& B : t->br) {
+    w.u64(B.P);
+    w.u64(B.num_weights);
+    w.u64(B.m);
+    w.vu64(B.widths);
+    // BranchParamsHost (params.rs:468-476)
+    w.u64(B.L);
+    for (int l = 0; l < B.L; ++l) w.vf32(B.params.data() + B.woff[l], (size_t)B.win[l] * B.widths[l]);
+    w.u64(B.L - 1);
+    for (int l = 0; l < B.L - 1; ++l) w.vf32(B.params.data() + B.boff[l], B.widths[l]);
+    w.vu64(B.widths);
+    w.u64(B.m);
+    w.f32(B.ows_reg_sum);
+    w.u64(B.ows_num);
+    // BranchPrecisionsHost (params.rs:192-199)
+    w.u64(B.L);
+    for (int l = 0; l < B.L; ++l) w.vf32(B.prec.data() + B.wpoff[l], B.wpn[l]);
+    w.u64(B.L - 1);
+    for (int l = 0; l < B.L - 1; ++l) w.vf32(B.prec.data() + B.bpoff + l, 1);
+    w.vf32(B.prec.data() + B.epoff, 1);
+    w.u32((uint32_t)B.act);  // ActivationFunction (activation_functions.rs:6-12)
+  }
+  w.f32(t->ob_eprec);  // OutputBias
+  w.f32(t->ob_prec);
+  w.f32(t->ob_bias);
+  w.u64(t->ns);  // TrainingStats
+  w.u64(t->nacc);
+  w.u64(t->nearly);
+  w.vf32(t->mse.data(), t->mse.size());
+  w.u8(0);  // mse_test: None
+  w.vf32(t->lpd.data(), t->lpd.size());
+  w.f32(t->lpd_rss);  // LogPosteriorDensity
+  w.f32(t->lpd_outw);
+  w.vf32(t->lpd_local.data(), t->lpd_local.size());
+  w.f32(t->g_eprec);  // GlobalParams
+  w.f32(t->g_oprec);
+  w.f32(t->g_reg_sum);
+  w.u64(t->g_num);
+  return w;  // branch_type: PhantomData, 0 bytes
+}
+
+int write_file(bann_net* t, const std::string& path) {
+  const Writer w = serialize(t);
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) return fail(t, BANN_E_ARG, "cannot open " + path + " for writing");
+  const size_t k = std::fwrite(w.b.data(), 1, w.b.size(), f);
+  const int rc = std::fclose(f);
+  if (k != w.b.size() || rc != 0) return fail(t, BANN_E_ARG, "short write to " + path);
+  return BANN_OK;
+}
+
+int write_training_stats(bann_net* t, const std::string& dir) {  // train_stats.rs:83-87 (serde_json)
+  const std::string path = dir + "/training_stats";
+  FILE* f = std::fopen(path.c_str(), "w");
+  if (!f) return fail(t, BANN_E_ARG, "cannot open " + path);
+  std::fprintf(f, "{\"num_samples\":%llu,\"num_accepted\":%llu,\"num_early_rejected\":%llu,\"mse_train\":[",
+               (unsigned long long)t->ns, (unsigned long long)t->nacc, (unsigned long long)t->nearly);
+  for (size_t i = 0; i < t->mse.size(); ++i) std::fprintf(f, i ? ",%.9g" : "%.9g", t->mse[i]);
+  std::fprintf(f, "],\"mse_test\":null,\"lpd\":[");
+  for (size_t i = 0; i < t->lpd.size(); ++i) std::fprintf(f, i ? ",%.9g" : "%.9g", t->lpd[i]);
+  std::fprintf(f, "]}");
+  std::fclose(f);
+  return BANN_OK;
+}
+
+}  // namespace
+
+extern "C" int bann_net_create(bann_ctx* ctx, const bann_precision_hyperparams* hp, uint64_t seed, bann_net** out) {
+  if (!ctx || !out) return BANN_E_ARG;
+  *out = nullptr;
+  const int nb = bann_num_branches(ctx);
+  if (nb <= 0) return BANN_E_STATE;
+  bann_net* t = new bann_net();
+  t->ctx = ctx;
+  t->gen.seed(seed);
+  if (hp) t->hp = *hp;
+  else t->hp = bann_precision_hyperparams{0.001f, 1000.f, 0.001f, 1000.f, 0.001f, 1000.f};  // vague (params.rs:119-124)
+  t->br.resize(nb);
+  t->lpd_local.assign(nb, -INFINITY);
+  for (int b = 0; b < nb; ++b) {
+    Branch& B = t->br[b];
+    int w[64];
+    int rc = bann_branch_info(ctx, b, &B.m, &B.L, w, 64, &B.act, &B.prior);
+    if (rc < 0 || B.L < 2 || B.L > 64) {
+      delete t;
+      return rc < 0 ? rc : BANN_E_SHAPE;
+    }
+    if (B.prior == P_STD_NORMAL) {  // Net::train panics for StdNormalBranch (net.rs:167 -> std_normal_branch.rs:129)
+      delete t;
+      return BANN_E_ARG;
+    }
+    B.widths.assign(w, w + B.L);
+    B.win.resize(B.L);
+    B.woff.resize(B.L);
+    B.boff.resize(B.L - 1);
+    B.wpoff.resize(B.L);
+    B.wpn.resize(B.L);
+    int64_t o = 0, po = 0;
+    for (int l = 0; l < B.L; ++l) {
+      B.win[l] = l == 0 ? B.m : B.widths[l - 1];
+      B.woff[l] = o;
+      o += (int64_t)B.win[l] * B.widths[l];
+      B.wpoff[l] = po;
+      B.wpn[l] = is_ard(B.prior) && l < B.L - 1 ? B.win[l] : 1;
+      po += B.wpn[l];
+    }
+    B.num_weights = o;
+    for (int l = 0; l < B.L - 1; ++l) {
+      B.boff[l] = o;
+      o += B.widths[l];
+    }
+    B.P = o;
+    B.bpoff = po;
+    B.epoff = po + B.L - 1;
+    B.NP = B.epoff + 1;
+    if (B.P != bann_num_params(ctx, b) || B.NP != bann_num_precisions(ctx, b)) {
+      delete t;
+      return BANN_E_SHAPE;
+    }
+    B.params.resize(B.P);
+    B.prec.resize(B.NP);
+    if ((rc = bann_branch_get_params(ctx, b, B.params.data())) < 0 ||
+        (rc = bann_branch_get_precisions(ctx, b, B.prec.data())) < 0) {
+      delete t;
+      return rc;
+    }
+  }
+  // BlockNetCfg::build_net (architectures.rs:187-237): summed output-weight
+  // statistic and count, error precision 2, one output-layer precision
+  double reg = 0.0;
+  for (const Branch& B : t->br) {
+    reg += B.out_stat();
+    t->g_num += (uint64_t)B.win[B.L - 1];
+  }
+  t->g_reg_sum = (float)reg;
+  t->g_oprec = t->br[0].prec[t->br[0].out_prec_ix()];
+  *out = t;
+  return BANN_OK;
+}
+
+extern "C" int bann_net_destroy(bann_net* t) {
+  delete t;
+  return BANN_OK;
+}
+
+extern "C" const char* bann_net_last_error(const bann_net* t) { return t ? t->err.c_str() : "null net"; }
+
+extern "C" int bann_net_set_rng_hooks(bann_net* t, const bann_rng_hooks* hooks) {
+  if (!t) return BANN_E_ARG;
+  t->hooks = hooks ? *hooks : bann_rng_hooks{};
+  return BANN_OK;
+}
+
+extern "C" int bann_net_set_global(bann_net* t, float error_precision, float output_layer_precision, float output_bias,
+                                   float output_bias_precision) {
+  if (!t) return BANN_E_ARG;
+  if (!(error_precision > 0.f) || !(output_layer_precision > 0.f) || !(output_bias_precision > 0.f))
+    return fail(t, BANN_E_ARG, "precisions must be positive");
+  t->g_eprec = t->ob_eprec = error_precision;
+  t->g_oprec = output_layer_precision;
+  t->ob_bias = output_bias;
+  t->ob_prec = output_bias_precision;
+  return BANN_OK;
+}
+
+extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir) {
+  if (!t || !y || !cfg) return BANN_E_ARG;
+  if (cfg->hmc_integration_length < 1 || cfg->chain_length < 0 || cfg->burn_in < 0)
+    return fail(t, BANN_E_ARG, "bad MCMC configuration");
+  if (cfg->hmc_step_size_mode != BANN_STEP_IZMAILOV && cfg->hmc_step_size_mode != BANN_STEP_UNIFORM)
+    return fail(t, BANN_E_ARG, "the driver supports Izmailov and uniform step sizes");
+  t->n = n;
+  const int nb = (int)t->br.size();
+  std::string dir = outdir ? outdir : "";
+  if (!dir.empty() && !mkdir_p(dir + "/models")) return fail(t, BANN_E_ARG, "cannot create " + dir + "/models");
+
+  // initialize_stats (net.rs:158-171): residual = y - bias - sum_b f_b
+  t->residual.assign(y, y + n);
+  for (auto& r : t->residual) r -= t->ob_bias;
+  std::vector<float> pred(n), prev(n), mom;
+  for (int b = 0; b < nb; ++b) {
+    Branch& B = t->br[b];
+    cfg_update_global(t, B);
+    CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
+    const double others = B.ows_reg_sum - B.out_stat();  // from_cfg (branch_struct.rs:26)
+    CKB(bann_predict(t->ctx, b, pred.data()));
+    for (int64_t i = 0; i < n; ++i) t->residual[i] -= pred[i];
+    update_lpd(t, b, others);
+  }
+  record_perf(t);
+  if (!dir.empty() && cfg->burn_in == 0) {
+    const int rc = write_file(t, dir + "/models/0.bin");
+    if (rc) return rc;
+  }
+
+  std::vector<int> order(nb);
+  for (int b = 0; b < nb; ++b) order[b] = b;
+  double kout = t->hp.output_shape, sout = t->hp.output_scale;
+  for (int chain_ix = 1; chain_ix <= cfg->chain_length; ++chain_ix) {
+    for (int i = nb - 1; i >= 1; --i) {  // branch_ixs.shuffle (net.rs:257)
+      const int j = std::min(i, (int)std::floor(draw_uniform(t) * (i + 1)));
+      std::swap(order[i], order[j]);
+    }
+    for (int b : order) {
+      Branch& B = t->br[b];
+      cfg_update_global(t, B);
+      const double others = B.ows_reg_sum - B.out_stat();
+      // sample_error_precision (branch_sampler.rs:190-202): output-layer hyperparameters
+      B.prec[B.epoff] = (float)ridge_posterior(t, kout, sout, sum_sq(t->residual.data(), n), (double)n);
+      if (!cfg->fixed_param_precisions) {  // sample_param_precisions (173-188)
+        sample_prior_precisions(t, B);
+        const double total = others + B.out_stat();  // add_output_weight_summary_stat_to_global
+        B.prec[B.out_prec_ix()] = (float)(is_lasso(B.prior) ? lasso_posterior(t, kout, sout, total, (double)B.ows_num)
+                                                            : ridge_posterior(t, kout, sout, total, (double)B.ows_num));
+      }
+      CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
+      // net.rs:279-280: the branch is fitted to residual + its own prediction
+      CKB(bann_predict(t->ctx, b, prev.data()));
+      for (int64_t i = 0; i < n; ++i) t->residual[i] += prev[i];
+      CKB(bann_branch_set_target(t->ctx, b, t->residual.data()));
+      mom.resize(B.P);
+      for (auto& p : mom) p = (float)draw_normal(t);
+      const float u = (float)draw_uniform(t);
+      int32_t status = 0;
+      CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error,
+                        cfg->hmc_step_size_mode, cfg->hmc_step_size_factor, nullptr, mom.data(), 0, &u, &status,
+                        nullptr, nullptr, nullptr));
+      ++t->ns;  // TrainingStats::add_hmc_step_result (train_stats.rs:46-53)
+      if (status == BANN_ACCEPTED) ++t->nacc;
+      if (status == BANN_REJECTED_EARLY) ++t->nearly;
+      CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
+      if (status == BANN_ACCEPTED) {  // net.rs:292-300
+        CKB(bann_predict(t->ctx, b, pred.data()));
+        for (int64_t i = 0; i < n; ++i) t->residual[i] -= pred[i];
+        update_lpd(t, b, others);
+      } else {
+        for (int64_t i = 0; i < n; ++i) t->residual[i] -= prev[i];
+      }
+      // to_cfg + GlobalParams::update_from_branch_cfg (net.rs:303-305, params.rs:41-56)
+      B.ows_reg_sum = (float)(others + B.out_stat());
+      if (!(B.prec[B.epoff] >= 0.f) || !(B.prec[B.out_prec_ix()] >= 0.f) || !(B.ows_reg_sum >= 0.f))
+        return fail(t, BANN_E_STATE, "invalid global parameter after branch update (params.rs:42-54)");
+      t->g_eprec = B.prec[B.epoff];
+      t->g_oprec = B.prec[B.out_prec_ix()];
+      t->g_reg_sum = B.ows_reg_sum;
+      // output bias (net.rs:319-332)
+      t->ob_eprec = t->g_eprec;
+      double sr = 0.0;
+      for (int64_t i = 0; i < n; ++i) sr += (double)(t->residual[i] += t->ob_bias);
+      if (cfg->sampled_output_bias) {
+        // sample_prior_precision passes the prior SHAPE as the scale (net.rs:61-66)
+        const double bsq = (double)t->ob_bias * t->ob_bias;
+        t->ob_prec = (float)draw_gamma(t, kout + 0.5, 2.0 * kout / (2.0 + kout * bsq));
+        const double den = (double)n * t->ob_eprec + t->ob_prec;  // sample_bias (47-53)
+        t->ob_bias = (float)(t->ob_eprec / den * sr + std::sqrt(1.0 / den) * draw_normal(t));
+      } else {
+        t->ob_bias = (float)(sr / (double)n);  // set_to_maximum_likelihood (43-45)
+      }
+      for (int64_t i = 0; i < n; ++i) t->residual[i] -= t->ob_bias;
+    }
+    record_perf(t);
+    if (!dir.empty() && chain_ix >= cfg->burn_in) {
+      const int rc = write_file(t, dir + "/models/" + std::to_string(chain_ix) + ".bin");
+      if (rc) return rc;
+    }
+  }
+  if (!dir.empty()) return write_training_stats(t, dir);
+  return BANN_OK;
+}
+
+extern "C" int bann_net_summary(const bann_net* t, bann_train_summary* out) {
+  if (!t || !out) return BANN_E_ARG;
+  out->num_samples = t->ns;
+  out->num_accepted = t->nacc;
+  out->num_early_rejected = t->nearly;
+  out->num_records = (int32_t)t->mse.size();
+  out->mse_train_last = t->mse.empty() ? NAN : t->mse.back();
+  out->lpd_last = t->lpd.empty() ? NAN : t->lpd.back();
+  out->output_bias = t->ob_bias;
+  out->error_precision = t->g_eprec;
+  out->output_layer_precision = t->g_oprec;
+  out->output_reg_sum = t->g_reg_sum;
+  return BANN_OK;
+}
+
+extern "C" int bann_net_records(const bann_net* t, float* mse_train, float* lpd, int32_t cap) {
+  if (!t || cap < 0) return BANN_E_ARG;
+  const int32_t k = std::min<int32_t>(cap, (int32_t)t->mse.size());
+  for (int32_t i = 0; i < k; ++i) {
+    if (mse_train) mse_train[i] = t->mse[i];
+    if (lpd) lpd[i] = t->lpd[i];
+  }
+  return k;
+}
+
+extern "C" int bann_net_residual(const bann_net* t, float* out) {
+  if (!t || !out) return BANN_E_ARG;
+  if ((int64_t)t->residual.size() != t->n || t->n == 0) return BANN_E_STATE;
+  std::copy(t->residual.begin(), t->residual.end(), out);
+  return BANN_OK;
+}
+
+extern "C" int bann_net_save(const bann_net* t, const char* path) {
+  if (!t || !path) return BANN_E_ARG;
+  return write_file(const_cast<bann_net*>(t), path);
+}
+
+extern "C" int bann_net_load(bann_net* t, const char* path) {
+  if (!t || !path) return BANN_E_ARG;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return fail(t, BANN_E_ARG, std::string("cannot open ") + path);
+  std::vector<uint8_t> buf;
+  uint8_t chunk[1 << 16];
+  size_t k;
+  while ((k = std::fread(chunk, 1, sizeof(chunk), f)) > 0) buf.insert(buf.end(), chunk, chunk + k);
+  std::fclose(f);
+  Reader r{buf.data(), buf.size()};
+  bann_precision_hyperparams hp;
+  hp.dense_shape = r.f32();
+  hp.dense_scale = r.f32();
+  hp.summary_shape = r.f32();
+  hp.summary_scale = r.f32();
+  hp.output_shape = r.f32();
+  hp.output_scale = r.f32();
+  const uint64_t nb = r.u64();
+  if (!r.ok || nb != t->br.size() || r.u64() != nb) return fail(t, BANN_E_SHAPE, "branch count differs from the context");
+  std::vector<Branch> br = t->br;
+  for (Branch& B : br) {
+    const uint64_t P = r.u64(), nw = r.u64(), m = r.u64();
+    const auto lw = r.vu64();
+    if (!r.ok || P != (uint64_t)B.P || nw != (uint64_t)B.num_weights || m != (uint64_t)B.m || lw.size() != (size_t)B.L)
+      return fail(t, BANN_E_SHAPE, "branch shape differs from the context");
+    for (int l = 0; l < B.L; ++l)
+      if (lw[l] != (uint64_t)B.widths[l]) return fail(t, BANN_E_SHAPE, "layer widths differ from the context");
+    if (r.u64() != (uint64_t)B.L) return fail(t, BANN_E_SHAPE, "weights: layer count");
+    for (int l = 0; l < B.L; ++l) {
+      const auto v = r.vf32();
+      if (v.size() != (size_t)B.win[l] * B.widths[l]) return fail(t, BANN_E_SHAPE, "weights: layer size");
+      std::copy(v.begin(), v.end(), B.params.begin() + B.woff[l]);
+    }
+    if (r.u64() != (uint64_t)(B.L - 1)) return fail(t, BANN_E_SHAPE, "biases: layer count");
+    for (int l = 0; l < B.L - 1; ++l) {
+      const auto v = r.vf32();
+      if (v.size() != (size_t)B.widths[l]) return fail(t, BANN_E_SHAPE, "biases: layer size");
+      std::copy(v.begin(), v.end(), B.params.begin() + B.boff[l]);
+    }
+    r.vu64();  // layer_widths (again) and num_markers inside BranchParamsHost
+    r.u64();
+    B.ows_reg_sum = r.f32();
+    B.ows_num = r.u64();
+    if (r.u64() != (uint64_t)B.L) return fail(t, BANN_E_SHAPE, "weight precisions: layer count");
+    for (int l = 0; l < B.L; ++l) {
+      const auto v = r.vf32();
+      if (v.size() != (size_t)B.wpn[l]) return fail(t, BANN_E_SHAPE, "weight precisions: size (prior differs?)");
+      std::copy(v.begin(), v.end(), B.prec.begin() + B.wpoff[l]);
+    }
+    if (r.u64() != (uint64_t)(B.L - 1)) return fail(t, BANN_E_SHAPE, "bias precisions: layer count");
+    for (int l = 0; l < B.L - 1; ++l) {
+      const auto v = r.vf32();
+      if (v.size() != 1) return fail(t, BANN_E_SHAPE, "bias precisions: size");
+      B.prec[B.bpoff + l] = v[0];
+    }
+    const auto ep = r.vf32();
+    if (ep.size() != 1) return fail(t, BANN_E_SHAPE, "error precision: size");
+    B.prec[B.epoff] = ep[0];
+    if ((int)r.u32() != B.act) return fail(t, BANN_E_SHAPE, "activation differs from the context");
+  }
+  const float ob_e = r.f32(), ob_p = r.f32(), ob_b = r.f32();
+  const uint64_t ns = r.u64(), na = r.u64(), ne = r.u64();
+  const auto mse = r.vf32();
+  if (r.u8() != 0) r.vf32();  // mse_test
+  const auto lpd = r.vf32();
+  const float l_rss = r.f32(), l_out = r.f32();
+  const auto l_loc = r.vf32();
+  const float ge = r.f32(), go = r.f32(), gr = r.f32();
+  const uint64_t gn = r.u64();
+  if (!r.ok || r.pos != r.n || l_loc.size() != nb) return fail(t, BANN_E_SHAPE, "truncated or malformed model file");
+  for (size_t b = 0; b < br.size(); ++b) {
+    CKB(bann_branch_set_params(t->ctx, (int32_t)b, br[b].params.data()));
+    CKB(bann_branch_set_precisions(t->ctx, (int32_t)b, br[b].prec.data()));
+  }
+  t->br = std::move(br);
+  t->hp = hp;
+  t->ob_eprec = ob_e;
+  t->ob_prec = ob_p;
+  t->ob_bias = ob_b;
+  t->ns = ns;
+  t->nacc = na;
+  t->nearly = ne;
+  t->mse = mse;
+  t->lpd = lpd;
+  t->lpd_rss = l_rss;
+  t->lpd_outw = l_out;
+  t->lpd_local = l_loc;
+  t->g_eprec = ge;
+  t->g_oprec = go;
+  t->g_reg_sum = gr;
+  t->g_num = gn;
+  return BANN_OK;
+}

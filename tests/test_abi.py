@@ -2,6 +2,7 @@
 exports every symbol include/bann.h declares; the Python binding covers them
 all; no compute is called (no GPU here)."""
 import ctypes
+import glob
 import os
 import re
 import subprocess
@@ -9,19 +10,23 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "bann.h")
+HEADERS = sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
 LIB = os.path.join(ROOT, "rs-bann_amd", "librsbann_amd.so")
 
 
 def header_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(bann_[a-z_0-9]+)\s*\(", txt)))
+    """every function declared in include/*.h (bann.h, bann_net.h)"""
+    fns = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        fns |= set(re.findall(r"\b(bann_[a-z_0-9]+)\s*\(", txt))
+    return sorted(fns)
 
 
 def test_header_parses():
     fns = header_functions()
-    assert "bann_ctx_create" in fns and "bann_hmc_step" in fns and len(fns) >= 30
+    assert len(HEADERS) >= 2
+    assert "bann_ctx_create" in fns and "bann_hmc_step" in fns and "bann_net_train" in fns and len(fns) >= 40
 
 
 @pytest.fixture(scope="module")
