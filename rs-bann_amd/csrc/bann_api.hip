@@ -57,6 +57,7 @@ struct bann_ctx {
   std::vector<BranchHost> br;
   bool finalized = false;
   bool fused_enabled = true;
+  bool wide_bf16 = false;  // wx kernel: hidden GEMMs on bf16 MFMA (opt-in, reduced precision)
   int32_t nfrag = 0, max_splits = 1;
   int64_t packed_bytes = 0, total_p = 0;
   // device buffers
@@ -261,9 +262,11 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       p.max_p_generic = std::max(p.max_p_generic, h.P);
       continue;
     }
-    const int grp = ((h.L - 2) * 5 + h.act) * 3 + (h.dev.nchunks < 8 ? 0 : h.dev.nchunks == 8 ? 1 : 2);
+    const bool wide = h.dev.fused == 2;
+    const int grp = wide ? BANN_WIDE_GROUP0 + h.act
+                         : ((h.L - 2) * 5 + h.act) * 3 + (h.dev.nchunks < 8 ? 0 : h.dev.nchunks == 8 ? 1 : 2);
     const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
-    const int ns = h.dev.nsplits;
+    const int ns = wide ? h.dev.nsplits / 4 : h.dev.nsplits;
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
       GradItem it;
       it.branch = b;
@@ -310,10 +313,15 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 
 // gradient (partials) of every branch in the plan at the current theta
 static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
-  for (int g = 0; g < BANN_NGROUPS; ++g)
-    if (!p.items[g].empty())
+  for (int g = 0; g < BANN_NGROUPS; ++g) {
+    if (p.items[g].empty()) continue;
+    if (g >= BANN_WIDE_GROUP0)
+      launch_fused_grad_wx(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), g - BANN_WIDE_GROUP0,
+                           ctx->wide_bf16 ? 1 : 0, write_pred, ctx->stream);
+    else
       launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 15 + 2, (g / 3) % 5,
                         g % 3 == 1, write_pred, ctx->stream);
+  }
   if (!p.generic.empty())
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
   CK(hipGetLastError());
@@ -537,12 +545,29 @@ extern "C" int64_t bann_num_precisions(const bann_ctx* ctx, int32_t b) {
   if (!ctx || b < 0 || b >= (int32_t)ctx->br.size()) return BANN_E_ARG;
   return ctx->br[b].nprec;
 }
+extern "C" int bann_branch_info(const bann_ctx* ctx, int32_t b, int32_t* m, int32_t* num_layers, int32_t* widths_out,
+                                int32_t widths_cap, int32_t* activation, int32_t* prior) {
+  if (!ctx || b < 0 || b >= (int32_t)ctx->br.size()) return BANN_E_ARG;
+  const BranchHost& h = ctx->br[b];
+  if (m) *m = h.m;
+  if (num_layers) *num_layers = h.L;
+  if (widths_out)
+    for (int l = 0; l < h.L && l < widths_cap; ++l) widths_out[l] = h.widths[l];
+  if (activation) *activation = h.act;
+  if (prior) *prior = h.prior;
+  return BANN_OK;
+}
 extern "C" int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b) {
   if (!check_branch(ctx, b)) return BANN_E_ARG;
   return ctx->br[b].dev.fused;
 }
 extern "C" const char* bann_fused_kernel_name(void) { return fused_kernel_family(); }
 
+extern "C" int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled) {
+  if (!ctx) return BANN_E_ARG;
+  ctx->wide_bf16 = enabled != 0;
+  return BANN_OK;
+}
 extern "C" int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled) {
   if (!ctx) return BANN_E_ARG;
   if (ctx->finalized) return fail(ctx, BANN_E_STATE, "set before bann_finalize");
@@ -570,6 +595,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     bool ok = ctx->fused_enabled && h.L >= 2 && h.L <= 4 && d.nchunks <= BANN_FUSED_MAXCH;
     for (int l = 0; l < h.L; ++l) ok = ok && h.widths[l] <= BANN_FUSED_MAXW;
     d.fused = ok ? 1 : 0;
+    // wide branches (one hidden layer up to 32 x 32, m <= 256): the wx kernel
+    if (!ok && ctx->fused_enabled && h.L == 3 && d.nchunks <= BANN_WIDE_MAXCH && h.widths[0] <= BANN_WIDE_MAXW &&
+        h.widths[1] <= BANN_WIDE_MAXW)
+      d.fused = 2;
     if (d.fused) total_frags += ctx->nfrag;
   }
   int64_t target_items = 1024;  // fewer, longer items: -1..2 % (prologue + barrier skew)
@@ -599,6 +628,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     BranchDev& d = h.dev;
+    if (d.fused == 2 && !(ctx->u2 && fused_u2_layout())) d.fused = 0;  // wx reads the 2-bit tile image only
     if (d.fused && ctx->u2 && d.nchunks <= 8) {  // the register-staged kernel serves <= 8 chunks
       d.x_off = x2_off;  // byte offset into the 2-bit buffer: [tile][chunk][64 lanes][16 B]
       x2_off += ntile * d.nchunks * 1024;
@@ -607,7 +637,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
       x_off += (int64_t)ctx->nfrag * d.nchunks * 1024;
     }
     d.dig_off = dig_off;
-    if (d.fused) dig_off += (int64_t)d.nchunks * 1024;
+    if (d.fused) dig_off += (int64_t)d.nchunks * 1024 * (d.fused == 2 ? 8 : 1);
     d.p_off = p_off;
     p_off += h.P;
     d.mk_off = mk_off;
@@ -615,10 +645,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     d.y_off = (int64_t)b * n;
     d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
     d.nsplits = (int32_t)std::min<int64_t>(d.nsplits, ntile);
+    if (d.fused) items += d.nsplits;
+    if (d.fused == 2) d.nsplits *= 4;  // wx: every wave of an item writes its own slab
     max_splits = std::max(max_splits, d.nsplits);
     d.part_off = part_off;
     part_off += (int64_t)d.nsplits * h.P;
-    if (d.fused) items += d.nsplits;
     d.scr_off = scr_off;
     if (!d.fused) {
       int64_t o = 0;

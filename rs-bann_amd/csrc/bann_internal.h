@@ -6,6 +6,8 @@
 
 #define BANN_MAXL 8          // max layers per branch (hidden + summary + output)
 #define BANN_FUSED_MAXW 4    // fused kernel: every layer width <= 4
+#define BANN_WIDE_MAXW 32    // wide fused kernel (wx): one hidden layer, W, S <= 32
+#define BANN_WIDE_MAXCH 2    // wide fused kernel: m_b <= 128
 #define BANN_FUSED_MAXCH 16  // fused kernel: <= 16 marker chunks of 64 (m_b <= 1024)
 #define BANN_CHUNK 64        // markers per chunk (one 16x16x64 i8 MFMA K-step)
 #define BANN_FRAG 16         // individuals per fragment (MFMA N)
@@ -30,7 +32,7 @@ struct BranchDev {
   int32_t prior;      // bann_prior
   int32_t P;          // num params
   int32_t nsplits;    // row splits (partial slabs)
-  int32_t fused;      // 1 = fused kernel path
+  int32_t fused;      // 1 = fused kernel path (widths <= 4), 2 = wide fused kernel (wx), 0 = generic
   int32_t widths[BANN_MAXL];  // out width of each layer (last = 1)
   int32_t win[BANN_MAXL];     // in width of each layer (win[0] = m)
   int32_t woff[BANN_MAXL];    // param_vec offset of W_l
@@ -51,8 +53,8 @@ struct GradItem {
 
 // Per-branch derived constants of the fused path (rewritten after every position update).
 struct FusedConst {
-  float scale[BANN_FUSED_MAXW];  // power-of-two scale of the W0/sigma digits per column
-  float c0[BANN_FUSED_MAXW];     // b0_k - sum_j mu_j W0_jk / sigma_j
+  float scale[BANN_WIDE_MAXW];  // power-of-two scale of the W0/sigma digits per column
+  float c0[BANN_WIDE_MAXW];     // b0_k - sum_j mu_j W0_jk / sigma_j
 };
 
 struct DevState {
@@ -108,7 +110,9 @@ void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp
 void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
                        int32_t act, int full8, int write_pred, hipStream_t s);
 // fused launch groups: ((L - 2) * 5 + activation) * 3 + (nchunks < 8 ? 0 : nchunks == 8 ? 1 : 2), L in [2, 4]
-#define BANN_NGROUPS 45
+// + 5 wide groups (one per activation): BANN_WIDE_GROUP0 + activation
+#define BANN_WIDE_GROUP0 45
+#define BANN_NGROUPS 50
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
@@ -122,6 +126,8 @@ int fused_u2_layout();              // 1: fx tile-row image (launch_pack_branch_
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
                            int32_t nchunks, int32_t ntile, hipStream_t s);  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
+void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
+                          int write_pred, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, hipStream_t s);
 void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,

@@ -54,6 +54,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
   const float* mu = st.mu + bd.mk_off;
   const float* sg = st.sigma + bd.mk_off;
   const int m = bd.m, w0 = bd.widths[0];
+  const int NB = bd.fused == 2 ? 8 : 1;  // column blocks of 4 in the digit image (wide kernel: 8)
   uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
   for (int k = 0; k < w0; ++k) {
     float mx = 0.f;
@@ -90,8 +91,8 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
       const int c = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        const int lane = 16 * grp + 4 * k + d;
-        dig[((int64_t)c * 64 + lane) * 16 + jj] = (uint8_t)q[d];
+        const int lane = 16 * grp + 4 * (k & 3) + d;
+        dig[(((int64_t)c * NB + (k >> 2)) * 64 + lane) * 16 + jj] = (uint8_t)q[d];
       }
     }
   }

@@ -76,7 +76,26 @@ CONFIGS = [
     dict(n=400, m=60, widths=[8, 8, 1], act="tanh", prior="ridge_ard"),
     dict(n=1000, m=100, widths=[50, 50, 1], act="tanh", prior="ridge_ard"),
     dict(n=1, m=3, widths=[2, 1], act="tanh", prior="ridge_base"),
+    # wide kernel (one hidden layer, W, S <= 32, m <= 128): C5's 32 x 32 at m = 125, ragged widths
+    dict(n=1000, m=125, widths=[32, 32, 1], act="tanh", prior="ridge_ard"),
+    dict(n=333, m=77, widths=[17, 9, 1], act="relu", prior="lasso_ard"),
+    dict(n=500, m=128, widths=[5, 3, 1], act="silu", prior="ridge_base"),
+    dict(n=257, m=40, widths=[32, 7, 1], act="leaky_relu", prior="lasso_base"),
+    dict(n=100, m=64, widths=[12, 32, 1], act="identity", prior="std_normal"),
+    dict(n=65, m=1, widths=[6, 6, 1], act="tanh", prior="ridge_ard"),
 ]
+
+
+def expected_path(cfg, fused):
+    """the kernel family bann_finalize picks (bann_api.hip)"""
+    w, m = cfg["widths"], cfg["m"]
+    if not fused:
+        return "generic"
+    if max(w) <= 4 and m <= 1024 and len(w) <= 4:
+        return "fused"
+    if len(w) == 3 and max(w) <= 32 and m <= 128:
+        return "wide"
+    return "generic"
 
 
 def make_problem(cfg, seed):
@@ -107,10 +126,7 @@ def test_gradient_parity(Ctx, ci, fused):
     f = O.predict(br, X)
     y = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=cfg["n"])).astype(np.float32).astype(np.float64)
     ctx.set_target(0, y)
-    if fused and cfg["widths"][0] <= 4 and max(cfg["widths"]) <= 4 and cfg["m"] <= 1024 and len(cfg["widths"]) <= 4:
-        assert ctx.kernel_path(0) == "fused"
-    else:
-        assert ctx.kernel_path(0) == "generic"
+    assert ctx.kernel_path(0) == expected_path(cfg, fused)
     grad, rss = ctx.log_density_gradient(0)
     ogw, ogb, orss = O.log_density_gradient(br, X, y)
     gw, gb = layer_views(br, grad)
@@ -188,16 +204,18 @@ def test_gradient_deterministic_and_split_invariant(Ctx):
 
 
 # ----------------------------------------------------------------- HMC parity
+@pytest.mark.parametrize("widths", [[4, 4, 1], [32, 32, 1]])
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("prior", ["ridge_ard", "lasso_base", "std_normal"])
-def test_hmc_step_parity(Ctx, prior, fused):
+def test_hmc_step_parity(Ctx, prior, fused, widths):
     """hmc_step (branch_sampler.rs:1192-1299) with injected momentum, step sizes
-    and acceptance uniform: same trajectory, -H trace, status and end state."""
+    and acceptance uniform: same trajectory, -H trace, status and end state
+    (4-wide fused kernel, wide wx kernel, generic kernels)."""
     rng = np.random.default_rng(11)
     n, m, L = 600, 120, 6
     g = O.synthetic_genotypes(rng, n, m)
     snps = np.arange(m, dtype=np.int32)
-    br = f32_branch(O.random_branch(rng, m, [4, 4, 1], prior=prior, act="tanh"))
+    br = f32_branch(O.random_branch(rng, m, widths, prior=prior, act="tanh"))
     ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(n))], fused=fused)
     X = oracle_inputs(ctx, g, snps)
     y = (O.predict(br, X) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
@@ -453,4 +471,66 @@ def test_c3_shape_branch_parity(Ctx):
         assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
     assert scalar_close(rss, orss), (rss, orss)
     assert norm_rel(ctx.predict(0), f) < TOL
+    ctx.close()
+
+
+# ------------------------------------------------------------- wide kernel (wx)
+def _wide_problem(Ctx, seed, n=2000, m=125, widths=(32, 32, 1), nb=3, act="tanh"):
+    rng = np.random.default_rng(seed)
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = [dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, list(widths), act=act)), y=None) for b in range(nb)]
+    ctx = build_context(Ctx, g, [dict(s, y=np.zeros(n)) for s in specs])
+    mu, sd = ctx.genotype_stats()
+    for b, s in enumerate(specs):
+        s["X"] = x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]])
+        f = O.predict(s["branch"], s["X"])
+        s["y"] = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=n)).astype(np.float32).astype(np.float64)
+        ctx.set_target(b, s["y"])
+    return ctx, specs
+
+
+def test_wide_packed_deterministic(Ctx):
+    """C5-shaped branches (m = 125, W = S = 32) packed in one launch: per-branch
+    parity, bitwise-reproducible fixed-order reductions, split invariance."""
+    ctx, specs = _wide_problem(Ctx, 41)
+    assert all(ctx.kernel_path(b) == "wide" for b in range(len(specs)))
+    for b, s in enumerate(specs):
+        grad, rss = ctx.log_density_gradient(b)
+        ogw, ogb, orss = O.log_density_gradient(s["branch"], s["X"], s["y"])
+        assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL, b
+        assert scalar_close(rss, orss)
+        g2, r2 = ctx.log_density_gradient(b)
+        assert np.array_equal(grad, g2) and rss == r2
+    many = ctx.predict_many([2, 0, 1])
+    for i, b in enumerate([2, 0, 1]):
+        assert norm_rel(many[i], O.predict(specs[b]["branch"], specs[b]["X"])) < TOL
+    g_ref = ctx.log_density_gradient(1)[0]
+    ctx.close()
+    os.environ["BANN_TARGET_ITEMS"] = "1"
+    try:
+        ctx, _ = _wide_problem(Ctx, 41)
+        g1 = ctx.log_density_gradient(1)[0]
+    finally:
+        del os.environ["BANN_TARGET_ITEMS"]
+    assert norm_rel(g1, g_ref) < 1e-6
+    ctx.close()
+
+
+def test_wide_bf16_hidden_gemm(Ctx):
+    """bann_set_hidden_gemm_bf16 (C5's bf16 hidden GEMM): the hidden-layer GEMMs
+    round their operands to bf16 (8-bit mantissa), so the gradient agrees with
+    the f32 oracle to ~1e-2 (norm-relative), not 1e-5; the masked layer stays
+    exact.  The f32 mode of the same context is parity-exact again."""
+    ctx, specs = _wide_problem(Ctx, 43, nb=2)
+    ctx.set_hidden_gemm_bf16(True)
+    s = specs[0]
+    grad, rss = ctx.log_density_gradient(0)
+    ogw, ogb, orss = O.log_density_gradient(s["branch"], s["X"], s["y"])
+    err = norm_rel(grad, O.param_vec(ogw, ogb))
+    assert 0 < err < 3e-2, err
+    assert scalar_close(rss, orss, 1e-2)
+    ctx.set_hidden_gemm_bf16(False)
+    grad, rss = ctx.log_density_gradient(0)
+    assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL
     ctx.close()
