@@ -37,9 +37,14 @@ CONFIGS = {
     "c3": (50_000, 500_000, 1000, [4, 4, 1]),
     "c2": (10_000, 128_000, 64, [4, 4, 1]),
     "small": (8_192, 64_000, 128, [4, 4, 1]),
+    # C5 (BASELINE.json configs[4]): 4k branches of 125 SNPs (500k-SNP panel),
+    # 100k individuals, W = S = 32: the wide kernel, hidden GEMMs on MFMA
+    "c5": (100_000, 500_000, 4000, [32, 32, 1]),
 }
 METRIC = "HMC leapfrog steps/sec (whole node), 50k indiv × 500k SNP × 1k branches"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TF = 157.3   # dense f32 MFMA = vector rate (MI355X_MICROARCH.md chip table)
+BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA (spec, no sparsity)
 
 
 def log(*a):
@@ -92,6 +97,8 @@ def main():
     ap.add_argument("--cpu-sample-branches", type=int, default=96)
     ap.add_argument("--cpu-sample-steps", type=int, default=16)
     ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--hidden-bf16", action="store_true",
+                    help="wide kernel: hidden GEMMs on bf16 MFMA (C5's bf16 vs fp32 comparison)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,7 +130,10 @@ def main():
     for k in range(nb):
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
-    assert all(ctx.kernel_path(k) == "fused" for k in range(nb))
+    wide = widths[0] > 4
+    assert all(ctx.kernel_path(k) == ("wide" if wide else "fused") for k in range(nb))
+    if args.hidden_bf16:
+        ctx.set_hidden_gemm_bf16(True)
     params, precs, out_ss = [], [], 0.0
     for k in range(nb):
         rng = np.random.default_rng(b0 + k)
@@ -210,9 +220,9 @@ def main():
     else:
         acc_all, nb_all = float(acc), float(nb)
 
-    workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W=S=4, RidgeARD, tanh, "
-                "Izmailov step sizes")
-    kernel_name = ctx.fused_kernel_name()
+    workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
+                "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else ""))
+    kernel_name = "k_fused_grad_wx" if wide else ctx.fused_kernel_name()
     # ---- kernel timing for the roofline (HIP events on the library stream) ----
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
     grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
@@ -228,7 +238,12 @@ def main():
     y_bytes = 4 * n * nb
     alg_bytes = x_bytes + y_bytes
     achieved = alg_bytes / (grad_ms * 1e-3) / 1e9
-
+    # wide branches: the dominant work is the hidden-layer GEMMs on MFMA --
+    # forward Z1 = A0 W1, error propagation err0 = delta1 W1^T and dW1 = A0^T delta1,
+    # 2 n W S flops each per branch (branch_sampler.rs:760-771, 844-866)
+    hidden_flops = 3 * 2 * n * widths[0] * widths[1] * nb
+    # the masked layer on the i8 MFMA: W0 and delta0 as 4 digits, forward + backward
+    i8_ops = 2 * 2 * n * m_b * 4 * widths[0] * nb
     # HBM traffic per gradient launch, from the committed PMC pass of the same
     # workload (tools/profile_round.sh; a --pmc run cannot time itself)
     traffic, traffic_src = None, None
@@ -267,8 +282,15 @@ def main():
             "config": {"workload": workload,
                        "n": n, "snps": M_total, "branches": B_total, "layer_widths": widths,
                        "branches_per_gpu": nb, "parallelism": f"branch-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "roofline": ({"bound": "mfma", "achieved": hidden_flops / (grad_ms * 1e-3) / 1e12,
+                          "peak": BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                          "frac": hidden_flops / (grad_ms * 1e-3) / 1e12 /
+                          (BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF),
+                          "basis": "hidden-layer GEMM flops 6 n W S per branch per launch",
+                          "i8_mfma_tops": i8_ops / (grad_ms * 1e-3) / 1e12,
+                          "hbm_GBps": achieved} if wide else
+                         {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": achieved / HBM_PEAK_GBS}) | {"traffic": traffic,
                          "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                          "kernel": kernel_name, "kernel_ms": grad_ms, "alg_bytes_per_launch": alg_bytes,
                          "packed_bytes_per_launch": ctx.packed_genotype_bytes,
