@@ -249,7 +249,7 @@ def main():
     traffic, traffic_src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         pm = json.load(open(f))
-        if world == 1 and pm.get("config") == workload and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
+        if world == 1 and pm.get("config", "").split(":")[0] == workload.split(":")[0] and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
             traffic, traffic_src = pm["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
             break
 

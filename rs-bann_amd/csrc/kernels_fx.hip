@@ -34,7 +34,10 @@
 //   * backward B operand (K = 64 individuals, N = 16 markers): one ds_read_b32
 //     gives lane (r, n) quads 4r .. 4r+3 of marker 16u + n; (w >> 2p) &
 //     0x03030303 holds individuals 16r + 4b + p (byte b), K slot 16r + 4p + b.
-//     The delta0 digit operand A is written in the same K order.
+//     Fields p = 1, 2 are used in place (w & 0x0C0C0C0C = 4 x code, w &
+//     0x30303030 = 16 x code); the delta0 digits of those individuals are taken
+//     at a 4^p smaller scale, so the MFMA sum is unchanged.  The delta0 digit
+//     operand A is written in the same K order.
 #include <stdlib.h>
 
 #include "activations.h"
@@ -454,8 +457,15 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         if (NCH != 0 || u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
     }
     v4u w;
+#if BANN_ABLATE & 8192
+    constexpr int kslot_sh = 0;
+#else
+    // this lane's individual sits in K-group p = g of the backward operand, whose
+    // genotype codes stay in place (x 4^p, p = 1, 2): pre-divide its digits by 4^p
+    const int kslot_sh = g == 1 ? 2 : g == 2 ? 4 : 0;
+#endif
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - (R[k] ? R[k] : 255));
+    for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - kslot_sh - (R[k] ? R[k] : 255));
     *reinterpret_cast<v4u*>(sd_w) = w;
 
     __builtin_amdgcn_sched_barrier(0);
@@ -475,8 +485,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         const uint32_t wv = wq[u % PD];
         if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+#if BANN_ABLATE & 8192
         const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u),
                            (int)((wv >> 4) & 0x03030303u), (int)((wv >> 6) & 0x03030303u)};
+#else
+        // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
+        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
+                           (int)((wv >> 6) & 0x03030303u)};
+#endif
 #if BANN_ABLATE & 2
         acc[u] += Bv ^ A;
 #else
