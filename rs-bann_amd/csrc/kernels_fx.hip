@@ -73,6 +73,14 @@ __device__ __forceinline__ float comb4(v4i d) {  // sum_d D_d 2^(-7 d)
   return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
 }
 
+// 2^21 x value of digit sums G, rounded once: the low digit sums grow past 2^24
+// over an item's tiles (in-place fields weigh up to 48), where comb4's
+// per-digit float conversion would round each one
+__device__ __forceinline__ float comb4_exact(v4i G) {
+  const int64_t N = ((int64_t)G[0] << 21) + ((int64_t)G[1] << 14) + ((int64_t)G[2] << 7) + (int64_t)G[3];
+  return (float)N;
+}
+
 // value(G) * 2^-sh for digit sums G (digit d weighs 2^(-7 d)), sh >= 0: form
 // N = G0 2^21 + G1 2^14 + G2 2^7 + G3 in int64 (|G_d| < 2^24), shift it, and
 // re-split into 7-bit digits (exact up to the dropped low bits, < 2^-21 of the
@@ -88,11 +96,26 @@ __device__ __forceinline__ v4i shr_digits(v4i G, int sh) {
 __device__ __forceinline__ uint32_t digits4_fx(float x, int e) {
   const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
   const uint32_t u = (uint32_t)V;
+#if BANN_ABLATE & 16384
   uint32_t w = __builtin_amdgcn_ubfe(u, 21, 8);
   w |= __builtin_amdgcn_ubfe(u, 14, 7) << 8;
   w |= __builtin_amdgcn_ubfe(u, 7, 7) << 16;
   w |= (u & 127u) << 24;
   return w;
+#else
+  // three bfe + three v_lshl_or_b32 + one and (the compiler's mask form takes 8)
+  uint32_t w, t;
+  asm("v_bfe_u32 %0, %2, 21, 8\n\t"
+      "v_bfe_u32 %1, %2, 14, 7\n\t"
+      "v_lshl_or_b32 %0, %1, 8, %0\n\t"
+      "v_bfe_u32 %1, %2, 7, 7\n\t"
+      "v_lshl_or_b32 %0, %1, 16, %0\n\t"
+      "v_and_b32 %1, 0x7f, %2\n\t"
+      "v_lshl_or_b32 %0, %1, 24, %0"
+      : "=&v"(w), "=&v"(t)
+      : "v"(u));
+  return w;
+#endif
 }
 
 __device__ __forceinline__ void swap32(float& a, float& b) {
@@ -563,7 +586,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     float* red = reinterpret_cast<float*>(&s_x[wave][0][0]);
 #pragma unroll
     for (int u = 0; u < 32; ++u)
-      if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4(acc[u]), Rl - 132) : 0.f;
+      if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4_exact(acc[u]), Rl - 153) : 0.f;
   }
   __syncthreads();
   float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
