@@ -31,7 +31,7 @@ upd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trac
            int(x["Grid_Size_X"]) for x in trace if "k_update" in x["Kernel_Name"])]
 
 
-def pmc_bytes(sub, counter):
+def pmc_bytes(sub, counter, pick=statistics.median):
     f = find(sub, "*counter_collection.csv")
     rows = list(csv.DictReader(open(f)))
     per = {}
@@ -43,17 +43,21 @@ def pmc_bytes(sub, counter):
     vals = [v for g, v in per.values()]
     gmax = max(g for g, v in per.values())
     vals = [v for g, v in per.values() if g == gmax]
-    return statistics.median(vals) * 1024.0  # rocprofv3 reports KB
+    return pick(vals) * 1024.0  # rocprofv3 reports KB
 
 
 fetch = pmc_bytes("fetch", "FETCH_SIZE") * 2.0   # gfx950: FETCH_SIZE counts 1/2 of wide streaming reads
-write = pmc_bytes("write", "WRITE_SIZE")
+# the steady-state leapfrog launch writes only the partial slabs; the first and
+# last launch of a trajectory also write the n predictions per branch (4 n B)
+write = pmc_bytes("write", "WRITE_SIZE", min)
+write_pred = pmc_bytes("write", "WRITE_SIZE", max)
 pmc = {"kernel": full[0]["Kernel_Name"], "config": bench["config"]["workload"],
        "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
-       "traffic_bytes_per_launch": fetch + write,
+       "traffic_bytes_per_launch": fetch + write, "write_bytes_trajectory_end_launch": write_pred,
        "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
        "note": "FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md HBM), WRITE_SIZE as reported; "
-               "median over the full-branch-set launches of a separate --pmc pass"}
+               "fetch: median over the full-branch-set launches of a separate --pmc pass; write: the steady-state "
+               "leapfrog launch (min; the trajectory's first and last launch also write predictions)"}
 json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
 
 with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
@@ -67,7 +71,8 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
     f.write(f"| k_update (full set) | {len(upd)} | {statistics.mean(upd):.3f} | {statistics.median(upd):.3f} | "
             f"{min(upd):.3f} |\n\n")
     f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.3f} ms\n\n")
-    f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB; "
+    f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB "
+            f"({write_pred/1e9:.4f} GB at a trajectory's first/last launch, predictions included); "
             f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
     f.write(f"achieved (algorithmic bytes / median launch): "
             f"{pmc['alg_bytes_per_launch'] / (statistics.median(dur) * 1e-3) / 1e9:.0f} GB/s\n\n")
