@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--cpu-sample-branches", type=int, default=96)
     ap.add_argument("--cpu-sample-steps", type=int, default=16)
     ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--emulate-shard", type=int, default=0,
+                    help="profiling only: run rank 0's shard of an N-GPU job on this one GPU, no collective")
     ap.add_argument("--hidden-bf16", action="store_true",
                     help="wide kernel: hidden GEMMs on bf16 MFMA (C5's bf16 vs fp32 comparison)")
     args = ap.parse_args()
@@ -120,7 +122,7 @@ def main():
 
     n, M_total, B_total, widths = CONFIGS[args.config]
     m_b = M_total // B_total
-    b0, b1 = shard_ranges([m_b] * B_total, world)[rank]   # contiguous, balanced by markers
+    b0, b1 = shard_ranges([m_b] * B_total, max(world, args.emulate_shard))[rank]   # contiguous, balanced by markers
     nb = b1 - b0
 
     t_setup = time.time()
@@ -249,7 +251,7 @@ def main():
     traffic, traffic_src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         pm = json.load(open(f))
-        if world == 1 and pm.get("config", "").split(":")[0] == workload.split(":")[0] and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
+        if world == 1 and not args.emulate_shard and pm.get("config", "").split(":")[0] == workload.split(":")[0] and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
             traffic, traffic_src = pm["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
             break
 
@@ -299,6 +301,8 @@ def main():
             "accept_rate": acc_all / nb_all,
             "setup_s": setup_s,
         }
+        if args.emulate_shard:
+            out["emulated_shard_of"] = args.emulate_shard   # not a whole-job number: one rank's shard
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

@@ -623,6 +623,28 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     ctx->u2 = flag == 0;
   }
   const int64_t ntile = (ctx->nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
+  // Splits of the 4-wide fused (fx) branches: whole rounds of resident
+  // workgroups.  All items of a packed launch are equally long, so a launch
+  // costs ceil(items / slots) rounds of (per-item prologue/epilogue + tiles per
+  // wave); choose the split count minimising that (e.g. 125 branches on one GPU
+  // of an 8-GPU shard: 4 splits = 500 items in one round, where the
+  // 1024-item target gave 9 splits = 1125 items in 3 partly empty rounds).
+  int32_t fx_splits = 0;
+  if (!getenv("BANN_TARGET_ITEMS") && !getenv("BANN_MIN_FRAGS")) {
+    int64_t nfx = 0;
+    for (auto& h : ctx->br) nfx += h.dev.fused == 1 ? 1 : 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int64_t slots = 2 * (int64_t)cus;  // k_fused_grad_fx: two workgroups per CU
+    double best = 0.0;
+    for (int32_t sp = 1; nfx > 0 && sp <= 64 && 4 * sp <= ntile; ++sp) {
+      const int64_t rounds = (nfx * sp + slots - 1) / slots;
+      const int64_t per_wave = (ntile + 4 * sp - 1) / (4 * sp);
+      const double cost = (double)rounds * (2.0 + (double)per_wave);  // ~2 tiles of prologue + epilogue
+      if (fx_splits == 0 || cost < best) best = cost, fx_splits = sp;
+    }
+  }
   int64_t x_off = 0, x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
@@ -644,6 +666,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     mk_off += h.m;
     d.y_off = (int64_t)b * n;
     d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
+    if (d.fused == 1 && fx_splits > 0) d.nsplits = fx_splits;
     d.nsplits = (int32_t)std::min<int64_t>(d.nsplits, ntile);
     if (d.fused) items += d.nsplits;
     if (d.fused == 2) d.nsplits *= 4;  // wx: every wave of an item writes its own slab
@@ -1135,7 +1158,7 @@ extern "C" int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms
     if (rc) return rc;
   }
   CK(hipEventRecord(e1, ctx->stream));
-  for (int i = 0; i < iters; ++i) launch_update(ctx->st, ctx->lf.d_all, nb, MODE_GRAD, 0, ctx->stream);
+  for (int i = 0; i < iters; ++i) launch_update(ctx->st, ctx->lf.d_all, nb, MODE_PROFILE, 1, ctx->stream);
   CK(hipEventRecord(e2, ctx->stream));
   CK(hipEventSynchronize(e2));
   float t01 = 0.f, t12 = 0.f;

@@ -13,7 +13,7 @@
 #define BANN_FRAG 16         // individuals per fragment (MFMA N)
 #define BANN_TILE_FRAGS 4    // fragments per fused-kernel tile (64 individuals)
 
-enum { MODE_GRAD = 0, MODE_INIT = 1, MODE_STEP = 2, MODE_LAST = 3 };
+enum { MODE_GRAD = 0, MODE_INIT = 1, MODE_STEP = 2, MODE_LAST = 3, MODE_PROFILE = 4 };
 enum { ST_RUNNING = -1, ST_ACCEPTED = 0, ST_REJECTED = 1, ST_REJECTED_EARLY = 2 };
 
 // Per-branch descriptor (device resident, one per branch).

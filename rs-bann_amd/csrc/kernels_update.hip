@@ -49,6 +49,10 @@ __device__ float block_max(float v, float* red) {
 // W0 the power-of-two scale s_k, the four signed 7-bit digits of
 // (W0_jk / sigma_j) / s_k in the MFMA A-operand layout, and c0_k.
 __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& bd, double* redd, float* redf) {
+  (void)redd;
+  (void)redf;
+  __shared__ float s_mx[4][UPD_THREADS / 64];
+  __shared__ double s_cs[4][UPD_THREADS / 64];
   const float* W0 = st.theta + bd.p_off + bd.woff[0];
   const float* b0 = st.theta + bd.p_off + bd.boff[0];
   const float* mu = st.mu + bd.mk_off;
@@ -56,97 +60,179 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
   const int m = bd.m, w0 = bd.widths[0];
   const int NB = bd.fused == 2 ? 8 : 1;  // column blocks of 4 in the digit image (wide kernel: 8)
   uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
-  for (int k = 0; k < w0; ++k) {
-    float mx = 0.f;
-    double cs = 0.0;
+  const int wv = threadIdx.x >> 6;
+  // four columns per pass: their max |W0/sigma| and mu . (W0/sigma) in one
+  // combined reduction (one barrier pair per four columns)
+  for (int k0 = 0; k0 < w0; k0 += 4) {
+    const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    double cs[4] = {0.0, 0.0, 0.0, 0.0};
     for (int j = threadIdx.x; j < m; j += UPD_THREADS) {
-      const float wp = sg[j] > 0.f ? W0[k * m + j] / sg[j] : 0.f;
-      mx = fmaxf(mx, fabsf(wp));
-      cs += (double)mu[j] * (double)wp;
-    }
-    mx = block_max(mx, redf);
-    cs = block_sum(cs, redd);
-    // s = 2^e with max/s <= 127
-    float s = 1.f;
-    if (mx > 0.f) {
-      int e;
-      frexpf(mx / 127.f, &e);
-      s = ldexpf(1.f, e);
-    }
-    if (threadIdx.x == 0) {
-      st.fc[b].scale[k] = s;
-      st.fc[b].c0[k] = (float)((double)b0[k] - cs);
-    }
-    const double inv = 1.0 / (double)s;
-    for (int j = threadIdx.x; j < m; j += UPD_THREADS) {
-      const float wp = sg[j] > 0.f ? W0[k * m + j] / sg[j] : 0.f;
-      double v = (double)wp * inv;  // |v| <= 127, exact (power-of-two scale)
-      int8_t q[4];
+      const float sj = sg[j];
+      const double mj = (double)mu[j];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const double r = rint(v);
-        q[d] = (int8_t)r;
-        v = (v - r) * 128.0;
+      for (int q = 0; q < 4; ++q)
+        if (q < nk) {
+          const float wp = sj > 0.f ? W0[(k0 + q) * m + j] / sj : 0.f;
+          mx[q] = fmaxf(mx[q], fabsf(wp));
+          cs[q] += mj * (double)wp;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
+        cs[q] += __shfl_xor(cs[q], o);
       }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s_mx[q][wv] = mx[q];
+        s_cs[q][wv] = cs[q];
+      }
+    __syncthreads();
+    double inv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float M = s_mx[q][0];
+      double C = s_cs[q][0];
+      for (int w = 1; w < UPD_THREADS / 64; ++w) {
+        M = fmaxf(M, s_mx[q][w]);
+        C += s_cs[q][w];
+      }
+      // s = 2^e with max/s <= 127
+      float sc = 1.f;
+      if (M > 0.f) {
+        int e;
+        frexpf(M / 127.f, &e);
+        sc = ldexpf(1.f, e);
+      }
+      inv[q] = 1.0 / (double)sc;
+      if (threadIdx.x == 0 && q < nk) {
+        st.fc[b].scale[k0 + q] = sc;
+        st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
+      }
+    }
+    for (int j = threadIdx.x; j < m; j += UPD_THREADS) {
+      const float sj = sg[j];
       const int c = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int lane = 16 * grp + 4 * (k & 3) + d;
-        dig[(((int64_t)c * NB + (k >> 2)) * 64 + lane) * 16 + jj] = (uint8_t)q[d];
+      for (int q = 0; q < 4; ++q) {
+        if (q >= nk) continue;
+        const int k = k0 + q;
+        const float wp = sj > 0.f ? W0[k * m + j] / sj : 0.f;
+        double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
+        int8_t dq[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const double r = rint(v);
+          dq[d] = (int8_t)r;
+          v = (v - r) * 128.0;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int lane = 16 * grp + 4 * (k & 3) + d;
+          dig[(((int64_t)c * NB + (k >> 2)) * 64 + lane) * 16 + jj] = (uint8_t)dq[d];
+        }
       }
     }
   }
 }
 
-__global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32_t* __restrict__ blist, int mode,
-                                                        int step) {
-  __shared__ double redd[UPD_THREADS / 64];
-  __shared__ float redf[UPD_THREADS / 64];
-  const int b = blist[blockIdx.x];
-  const BranchDev bd = st.br[b];
-  const int P = bd.P;
-  const int64_t base = bd.p_off;
-  if ((mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
+// NV doubles summed over the workgroup in one pass (one barrier pair)
+template <int NV>
+__device__ void block_sum_n(double (&v)[NV], double* red) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q * (UPD_THREADS / 64) + w] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double t = 0.0;
+    for (int k = 0; k < UPD_THREADS / 64; ++k) t += red[q * (UPD_THREADS / 64) + k];
+    v[q] = t;
+  }
+}
 
-  // ---- rss and the log-density gradient (fixed-order split reduction) ----
+// Register-resident update of a small fused branch (P <= UPD_CAP * 256, m <= 512,
+// <= 4 first-layer columns: every C2/C3/C4 branch).  All global loads of the
+// step are issued up front (partials, theta, lambda, momentum, eps, theta0,
+// mu, sigma), the parameters stay in registers between the reduction and the
+// position step, and the W0-digit refresh reads the new W0 from LDS: two
+// memory latencies and two workgroup reductions per launch instead of about
+// seven dependent global round trips (the launch follows a genotype stream that
+// has evicted all of it from L2).  Same arithmetic as the general path below.
+#define UPD_CAP 8
+__device__ void update_small(const DevState& st, int b, const BranchDev& bd, int mode, bool prof, int step,
+                             double* redd, float* s_th) {
+  const int P = bd.P, m = bd.m, w0 = bd.widths[0];
+  const int64_t base = bd.p_off;
+  const int t = threadIdx.x;
+  // marker statistics for the refresh, prefetched
+  float mus[2], sgs[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = t + c * UPD_THREADS;
+    mus[c] = j < m ? st.mu[bd.mk_off + j] : 0.f;
+    sgs[c] = j < m ? st.sigma[bd.mk_off + j] : 0.f;
+  }
   double rss = 0.0;
   for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
   const float le = st.eprec[b];
   const bool lasso = (bd.prior == 2 || bd.prior == 3);
-  double ldp = 0.0;
-  for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
+  float th[UPD_CAP], gr[UPD_CAP], pm[UPD_CAP], ep[UPD_CAP], t0[UPD_CAP];
+  double sums[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < UPD_CAP; ++c) {
+    const int i = t + c * UPD_THREADS;
+    th[c] = gr[c] = pm[c] = ep[c] = t0[c] = 0.f;
+    if (i >= P) continue;
     float d = 0.f;
     for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
-    const float th = st.theta[base + i];
+    th[c] = st.theta[base + i];
     const float lm = st.lam[base + i];
-    const float sgn = th > 0.f ? 1.f : (th < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
-    const float reg = lasso ? lm * sgn : lm * th;
-    st.grad[base + i] = -(le * d + reg);
     const float ll = st.lamld[base + i];
-    ldp -= lasso ? (double)ll * fabs((double)th) : 0.5 * (double)ll * (double)th * (double)th;
+    pm[c] = st.mom[base + i];
+    ep[c] = st.eps[base + i];
+    if (mode == MODE_STEP || mode == MODE_LAST) t0[c] = st.theta0[base + i];
+    const float sgn = th[c] > 0.f ? 1.f : (th[c] < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
+    const float reg = lasso ? lm * sgn : lm * th[c];
+    gr[c] = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
+    if (!prof) st.grad[base + i] = gr[c];
+    sums[0] -= lasso ? (double)ll * fabs((double)th[c]) : 0.5 * (double)ll * (double)th[c] * (double)th[c];
+    if (mode == MODE_INIT) {
+      sums[1] += (double)pm[c] * (double)pm[c];
+    } else if (mode != MODE_GRAD) {  // second half step of this leapfrog step (momentum.rs:121-136)
+      pm[c] = pm[c] + ep[c] * 0.5f * gr[c];
+      sums[1] += (double)pm[c] * (double)pm[c];
+      sums[2] += ((double)th[c] - (double)t0[c]) * (double)pm[c];
+    }
   }
-  ldp = block_sum(ldp, redd);
-  const double ld = ldp - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
-
   if (mode == MODE_GRAD) {
-    if (threadIdx.x == 0) {
-      st.ld_out[b] = ld;
+    double v1[1] = {sums[0]};
+    block_sum_n<1>(v1, redd);
+    if (t == 0) {
+      st.ld_out[b] = v1[0] - (double)le * rss / 2.0;
       st.rss_out[b] = rss;
     }
     return;
   }
-  __syncthreads();  // grad visible block-wide
-
+  block_sum_n<3>(sums, redd);
+  const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
+  const double h = ld - 0.5 * sums[1];                   // -H (878-883)
   const int stride = st.lint + 1;
+  // what happens to theta: 0 = position step, 1 = restore theta0, 2 = keep
+  int act = 0;
   if (mode == MODE_INIT) {
-    double kin = 0.0;
-    for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
-      const float p = st.mom[base + i];
-      kin += (double)p * (double)p;
-    }
-    kin = 0.5 * block_sum(kin, redd);
-    if (threadIdx.x == 0) {
-      const double h = ld - kin;
+    if (t == 0) {
       st.h0[b] = h;
       st.htrace[(int64_t)b * stride] = h;
       st.status[b] = ST_RUNNING;
@@ -154,7 +240,210 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
       st.rss_out[b] = rss;
       st.ld_out[b] = ld;
     }
-    for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
+  } else {
+    const double h0 = st.h0[b];
+    const bool diverged = !prof && fabs(h - h0) > (double)st.max_dh;
+    if (!prof && t == 0) st.htrace[(int64_t)b * stride + step] = h;
+    if (diverged) {  // RejectedEarly (1264-1279)
+      act = 1;
+      if (t == 0) st.status[b] = ST_REJECTED_EARLY;
+    } else {
+      if (!prof && t == 0 && sums[2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;  // 1281-1284
+      if (mode == MODE_LAST) {  // Metropolis (928-962)
+        const double log_acc = h - h0;
+        const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
+        const bool accept = (double)st.uacc[b] < acc_p;
+        act = accept ? 2 : 1;
+        if (t == 0) {
+          st.status[b] = accept ? ST_ACCEPTED : ST_REJECTED;
+          st.ld_out[b] = ld;
+          st.rss_out[b] = rss;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < UPD_CAP; ++c) {
+    const int i = t + c * UPD_THREADS;
+    if (i >= P) continue;
+    float tn = th[c];
+    if (act == 0) {  // (next) first half step + position step (params.rs:728-738)
+      const float p = pm[c] + 0.5f * ep[c] * gr[c];
+      tn = th[c] + ep[c] * p;
+      if (prof) {
+        st.grad[base + i] = tn;  // same traffic, chain unchanged
+        tn = th[c];
+      } else {
+        st.mom[base + i] = p;
+        st.theta[base + i] = tn;
+        if (mode == MODE_INIT) st.theta0[base + i] = th[c];
+      }
+    } else {
+      if (mode != MODE_INIT && !prof) st.mom[base + i] = pm[c];  // the half-stepped momentum
+      if (act == 1) {
+        tn = t0[c];
+        st.theta[base + i] = tn;
+      }
+    }
+    s_th[i] = tn;
+  }
+  __syncthreads();
+  // ---- W0 digit refresh from the new W0 in LDS (the general refresh_fused_const) ----
+  const float* W0 = s_th + bd.woff[0];
+  const float* b0 = s_th + bd.boff[0];
+  float mx[4] = {0.f, 0.f, 0.f, 0.f};
+  double cs[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = t + c * UPD_THREADS;
+    if (j >= m) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < w0) {
+        const float wp = sgs[c] > 0.f ? W0[q * m + j] / sgs[c] : 0.f;
+        mx[q] = fmaxf(mx[q], fabsf(wp));
+        cs[q] += (double)mus[c] * (double)wp;
+      }
+  }
+  __shared__ float s_mx[4][UPD_THREADS / 64];
+  __shared__ double s_cs[4][UPD_THREADS / 64];
+  const int wv = t >> 6;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
+      cs[q] += __shfl_xor(cs[q], o);
+    }
+  if ((t & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s_mx[q][wv] = mx[q];
+      s_cs[q][wv] = cs[q];
+    }
+  __syncthreads();
+  double inv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float M = s_mx[q][0];
+    double C = s_cs[q][0];
+    for (int w = 1; w < UPD_THREADS / 64; ++w) {
+      M = fmaxf(M, s_mx[q][w]);
+      C += s_cs[q][w];
+    }
+    float sc = 1.f;  // s = 2^e with max/s <= 127
+    if (M > 0.f) {
+      int e;
+      frexpf(M / 127.f, &e);
+      sc = ldexpf(1.f, e);
+    }
+    inv[q] = 1.0 / (double)sc;
+    if (t == 0 && q < w0) {
+      st.fc[b].scale[q] = sc;
+      st.fc[b].c0[q] = (float)((double)b0[q] - C);
+    }
+  }
+  uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int j = t + c * UPD_THREADS;
+    if (j >= m) continue;
+    const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= w0) continue;
+      const float wp = sgs[c] > 0.f ? W0[q * m + j] / sgs[c] : 0.f;
+      double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
+      int8_t dq[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const double r = rint(v);
+        dq[d] = (int8_t)r;
+        v = (v - r) * 128.0;
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) dig[(((int64_t)ch * 64 + 16 * grp + 4 * q + d) * 16) + jj] = (uint8_t)dq[d];
+    }
+  }
+}
+
+// Per leapfrog step: ONE pass over the parameters computes the prior gradient,
+// the half-stepped momentum and every scalar of the step (log prior, kinetic
+// energy, U-turn dot product), with one combined workgroup reduction; a second
+// pass applies the position step (or the restore).  (The first version had a
+// reduction per scalar and re-read each array per phase: ~40 us per launch,
+// 18 % of a step at 125 branches per GPU.)  MODE_PROFILE repeats STEP's work
+// without changing the chain (bann_profile_session).
+__global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32_t* __restrict__ blist, int mode,
+                                                        int step) {
+  __shared__ double redd[4 * (UPD_THREADS / 64)];
+  __shared__ float redf[UPD_THREADS / 64];
+  const int b = blist[blockIdx.x];
+  const BranchDev bd = st.br[b];
+  const int P = bd.P;
+  const int64_t base = bd.p_off;
+  const bool prof = mode == MODE_PROFILE;
+  if (prof) mode = MODE_STEP;
+  if (!prof && (mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
+  if (bd.fused == 1 && P <= UPD_CAP * UPD_THREADS && bd.m <= 2 * UPD_THREADS && bd.widths[0] <= 4) {
+    __shared__ float s_th[UPD_CAP * UPD_THREADS];
+    update_small(st, b, bd, mode, prof, step, redd, s_th);
+    return;
+  }
+
+  // ---- rss (fixed-order split reduction) ----
+  double rss = 0.0;
+  for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
+  const float le = st.eprec[b];
+  const bool lasso = (bd.prior == 2 || bd.prior == 3);
+  // sums[0] = log prior (ridge_ard.rs:171-194 and the other priors), sums[1] =
+  // sum p^2 (momentum.rs:149-158; INIT: the drawn momentum, else the
+  // half-stepped one), sums[2] = sum (theta - theta0) . p (551-592)
+  double sums[3] = {0.0, 0.0, 0.0};
+  for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
+    float d = 0.f;
+    for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
+    const float th = st.theta[base + i];
+    const float lm = st.lam[base + i];
+    const float sgn = th > 0.f ? 1.f : (th < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
+    const float reg = lasso ? lm * sgn : lm * th;
+    const float gr = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
+    st.grad[base + i] = gr;
+    const float ll = st.lamld[base + i];
+    sums[0] -= lasso ? (double)ll * fabs((double)th) : 0.5 * (double)ll * (double)th * (double)th;
+    if (mode == MODE_INIT) {
+      const float p = st.mom[base + i];
+      sums[1] += (double)p * (double)p;
+    } else if (mode != MODE_GRAD) {  // second half step of this leapfrog step (momentum.rs:121-136)
+      const float p = st.mom[base + i] + st.eps[base + i] * 0.5f * gr;
+      if (!prof) st.mom[base + i] = p;
+      sums[1] += (double)p * (double)p;
+      sums[2] += ((double)th - (double)st.theta0[base + i]) * (double)p;
+    }
+  }
+  if (mode == MODE_GRAD) {
+    double v1[1] = {sums[0]};
+    block_sum_n<1>(v1, redd);
+    if (threadIdx.x == 0) {
+      st.ld_out[b] = v1[0] - (double)le * rss / 2.0;
+      st.rss_out[b] = rss;
+    }
+    return;
+  }
+  block_sum_n<3>(sums, redd);
+  const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
+  const double h = ld - 0.5 * sums[1];                   // -H = log density - K (878-883)
+  const int stride = st.lint + 1;
+  if (mode == MODE_INIT) {
+    if (threadIdx.x == 0) {
+      st.h0[b] = h;
+      st.htrace[(int64_t)b * stride] = h;
+      st.status[b] = ST_RUNNING;
+      st.uturn[b] = -1;
+      st.rss_out[b] = rss;
+      st.ld_out[b] = ld;
+    }
+    for (int i = threadIdx.x; i < P; i += UPD_THREADS) {  // first half step + full position step
       const float e = st.eps[base + i];
       const float th = st.theta[base + i];
       st.theta0[base + i] = th;
@@ -163,34 +452,26 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
       st.theta[base + i] = th + e * p;
     }
   } else {
-    // second half step of this leapfrog step, then -H (1249-1253)
-    double kin = 0.0;
-    for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
-      const float p = st.mom[base + i] + st.eps[base + i] * 0.5f * st.grad[base + i];
-      st.mom[base + i] = p;
-      kin += (double)p * (double)p;
-    }
-    kin = 0.5 * block_sum(kin, redd);
-    const double h = ld - kin;
     const double h0 = st.h0[b];
-    const bool diverged = fabs(h - h0) > (double)st.max_dh;
-    if (threadIdx.x == 0) st.htrace[(int64_t)b * stride + step] = h;
-    if (diverged) {  // RejectedEarly: restore the initial params (1277-1278)
+    const bool diverged = !prof && fabs(h - h0) > (double)st.max_dh;
+    if (!prof && threadIdx.x == 0) st.htrace[(int64_t)b * stride + step] = h;
+    if (diverged) {  // RejectedEarly: restore the initial params (1264-1279)
       for (int i = threadIdx.x; i < P; i += UPD_THREADS) st.theta[base + i] = st.theta0[base + i];
       if (threadIdx.x == 0) st.status[b] = ST_REJECTED_EARLY;
     } else {
-      // U-turn diagnostic (1281-1284): sum (theta - theta0) . p < 0
-      double nm = 0.0;
-      for (int i = threadIdx.x; i < P; i += UPD_THREADS)
-        nm += ((double)st.theta[base + i] - (double)st.theta0[base + i]) * (double)st.mom[base + i];
-      nm = block_sum(nm, redd);
-      if (threadIdx.x == 0 && nm < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;
-      if (mode == MODE_STEP) {
+      // U-turn diagnostic (1281-1284)
+      if (!prof && threadIdx.x == 0 && sums[2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;
+      if (mode == MODE_STEP) {  // next step's first half step + position step (params.rs:728-738)
         for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
           const float e = st.eps[base + i];
-          const float p = st.mom[base + i] + 0.5f * e * st.grad[base + i];
-          st.mom[base + i] = p;
-          st.theta[base + i] += e * p;
+          const float g = st.grad[base + i];
+          const float p = (prof ? st.mom[base + i] + st.eps[base + i] * 0.5f * g : st.mom[base + i]) + 0.5f * e * g;
+          if (prof) {
+            st.grad[base + i] = st.theta[base + i] + e * p;  // same traffic, chain unchanged
+          } else {
+            st.mom[base + i] = p;
+            st.theta[base + i] += e * p;
+          }
         }
       } else {  // MODE_LAST: Metropolis decision (accept_or_reject_hmc_state, 928-962)
         const double log_acc = h - h0;
