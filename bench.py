@@ -94,7 +94,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--step-factor", type=float, default=1.0)   # cli.rs:99-100 default
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-branches", type=int, default=96)
+    ap.add_argument("--cpu-sample-branches", type=int, default=96)   # capped at the config's branch count
     ap.add_argument("--cpu-sample-steps", type=int, default=16)
     ap.add_argument("--profile-iters", type=int, default=10)
     ap.add_argument("--emulate-shard", type=int, default=0,
@@ -133,7 +133,7 @@ def main():
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
     wide = widths[0] > 4
-    assert all(ctx.kernel_path(k) == ("wide" if wide else "fused") for k in range(nb))
+    assert all(ctx.kernel_path(k) == ("wide" if wide else ("fused" if m_b <= 512 else "fused_large")) for k in range(nb))
     if args.hidden_bf16:
         ctx.set_hidden_gemm_bf16(True)
     params, precs, out_ss = [], [], 0.0
@@ -224,7 +224,7 @@ def main():
 
     workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
                 "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else ""))
-    kernel_name = "k_fused_grad_wx" if wide else ctx.fused_kernel_name()
+    kernel_name = "k_fused_grad_wx" if wide else ("k_fused_grad_fx" if m_b <= 512 else "k_fused_grad_fxl")
     # ---- kernel timing for the roofline (HIP events on the library stream) ----
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
     grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
@@ -257,13 +257,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        c = cpu_baseline(n, m_b, widths, args.cpu_sample_branches, args.cpu_sample_steps)
+        sample_b = min(args.cpu_sample_branches, B_total)
+        c = cpu_baseline(n, m_b, widths, sample_b, args.cpu_sample_steps)
         if c is not None:
             cpu = {"value": c["branch_steps_per_s"] / B_total, "unit": "leapfrog steps/s",
                    "cores": c["threads"], "kind": "port",
-                   "sample": f"{args.cpu_sample_branches} branches x {args.cpu_sample_steps} leapfrog steps at "
+                   "sample": f"{sample_b} branches x {args.cpu_sample_steps} leapfrog steps at "
                              f"n={n}, m_b={m_b}, widths={widths} (C restatement of the reference op order, f32, "
-                             f"X read 3x per step), extrapolated x{B_total}/{args.cpu_sample_branches} branches; "
+                             f"X read 3x per step), extrapolated x{B_total}/{sample_b} branches; "
                              f"{c['seconds']:.1f}s of CPU work"}
 
     steps_per_s = args.steps / elapsed

@@ -199,10 +199,11 @@ int bann_synchronize(bann_ctx* ctx);
 int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms);
 
 /* ---------------- introspection for tests / profiling ---------------- */
-/* which gradient kernel serves branch b: 1 = fused single-pass kernel (every
- * width <= 4), 2 = wide fused kernel (one hidden layer, W, S <= 32, m <= 128:
- * masked layer on i8 MFMA, hidden GEMMs on f32 or bf16 MFMA), 0 = generic
- * multi-pass kernels */
+/* which gradient kernel serves branch b: 1 = fx fused single-pass kernel (every
+ * width <= 4, m <= 512), 3 = fxl (every width <= 4, 512 < m <= 4096: one wave
+ * per 512-marker block), 2 = wide fused kernel (one hidden layer, W, S <= 32,
+ * m <= 128: masked layer on i8 MFMA, hidden GEMMs on f32 or bf16 MFMA),
+ * 0 = generic kernels (any shape) */
 int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
 /* name of the fused gradient kernel family used for branches of <= 512 markers */
 const char* bann_fused_kernel_name(void);

@@ -31,14 +31,20 @@ struct BranchHost {
   BranchDev dev{};
 };
 
+// one packed gradient launch: every work item of one kernel instantiation
+struct LaunchGroup {
+  int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
+  int32_t L = 0, act = 0, nw = 1, full = 0;
+  std::vector<GradItem> items;
+  GradItem* d_items = nullptr;
+};
+
 struct Plan {
   std::vector<int32_t> all, generic;
-  std::vector<GradItem> items[BANN_NGROUPS];
-  int32_t nwaves[BANN_NGROUPS] = {};
+  std::vector<LaunchGroup> groups;
   int32_t max_p_generic = 0, max_p = 0;
   int32_t* d_all = nullptr;
   int32_t* d_gen = nullptr;
-  GradItem* d_items[BANN_NGROUPS] = {};
   bool owns = false;
 };
 
@@ -62,9 +68,7 @@ struct bann_ctx {
   int64_t packed_bytes = 0, total_p = 0;
   // device buffers
   BranchDev* d_br = nullptr;
-  int8_t* d_xpk = nullptr;
-  uint8_t* d_xu2 = nullptr;  // 2-bit packed genotypes of the fused branches (u2 format)
-  bool u2 = false;
+  uint8_t* d_xu2 = nullptr;  // 2-bit genotype tile images of every branch (u2t, kernels_fx.hip)
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;
@@ -125,7 +129,7 @@ static void free_plan(Plan& p) {
   if (p.owns) {
     dfree(p.d_all);
     dfree(p.d_gen);
-    for (auto& d : p.d_items) dfree(d);
+    for (auto& g : p.groups) dfree(g.d_items);
   }
   p = Plan{};
 }
@@ -133,9 +137,7 @@ static void free_plan(Plan& p) {
 static void refresh_state(bann_ctx* ctx) {
   DevState& s = ctx->st;
   s.br = ctx->d_br;
-  s.xpk = ctx->d_xpk;
   s.xu2 = ctx->d_xu2;
-  s.u2 = ctx->u2 ? 1 : 0;
   s.dig = ctx->d_dig;
   s.fc = ctx->d_fc;
   s.mu = ctx->d_mub;
@@ -251,31 +253,54 @@ static void step_bases(const BranchHost& h, std::vector<double>& out) {
 
 static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent) {
   free_plan(p);
-  p.all.assign(branches, branches + nb);
+  const int32_t nbr = (int32_t)ctx->br.size();
+  if (nb > nbr) return fail(ctx, BANN_E_ARG, "branch list longer than the branch set");
+  std::vector<char> seen(nbr, 0);
   for (int i = 0; i < nb; ++i) {
     const int b = branches[i];
-    if (b < 0 || b >= (int32_t)ctx->br.size()) return fail(ctx, BANN_E_SHAPE, "branch index out of range");
+    if (b < 0 || b >= nbr) return fail(ctx, BANN_E_SHAPE, "branch index out of range");
+    if (seen[b]) return fail(ctx, BANN_E_ARG, "duplicate branch in list");
+    seen[b] = 1;
+  }
+  p.all.assign(branches, branches + nb);
+  const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
     const BranchHost& h = ctx->br[b];
+    const BranchDev& d = h.dev;
     p.max_p = std::max(p.max_p, h.P);
-    if (!h.dev.fused) {
+    if (!d.fused) {
       p.generic.push_back(b);
       p.max_p_generic = std::max(p.max_p_generic, h.P);
       continue;
     }
-    const bool wide = h.dev.fused == 2;
-    const int grp = wide ? BANN_WIDE_GROUP0 + h.act
-                         : ((h.L - 2) * 5 + h.act) * 3 + (h.dev.nchunks < 8 ? 0 : h.dev.nchunks == 8 ? 1 : 2);
-    const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
-    const int ns = wide ? h.dev.nsplits / 4 : h.dev.nsplits;
+    LaunchGroup key;
+    key.kind = d.fused;
+    key.act = h.act;
+    if (d.fused == 1) {  // fx: (L, act, exactly 8 chunks)
+      key.L = h.L;
+      key.full = d.nchunks == 8;
+    } else if (d.fused == 3) {  // fxl: (L, act, waves, every wave 8 chunks)
+      key.L = h.L;
+      key.nw = (d.nchunks + 7) / 8;
+      key.full = d.nchunks == 8 * key.nw;
+    }
+    LaunchGroup* grp = nullptr;
+    for (auto& g : p.groups)
+      if (g.kind == key.kind && g.L == key.L && g.act == key.act && g.nw == key.nw && g.full == key.full) grp = &g;
+    if (!grp) {
+      p.groups.push_back(key);
+      grp = &p.groups.back();
+    }
+    const int ns = d.fused == 2 ? d.nsplits / 4 : d.nsplits;
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
       GradItem it;
       it.branch = b;
       it.split = s;
       it.frag_begin = (int32_t)(BANN_TILE_FRAGS * (ntile * s / ns));
       it.frag_end = (int32_t)std::min<int64_t>(nfrag, BANN_TILE_FRAGS * (ntile * (s + 1) / ns));
-      p.items[grp].push_back(it);
+      grp->items.push_back(it);
     }
-    p.nwaves[grp] = std::max(p.nwaves[grp], h.dev.nchunks);
   }
   if (persistent) {
     p.owns = true;
@@ -285,11 +310,10 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
     if (!p.generic.empty())
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
-    for (int g = 0; g < BANN_NGROUPS; ++g) {
-      if (p.items[g].empty()) continue;
-      CK(dalloc(&p.d_items[g], (int64_t)p.items[g].size()));
-      CK(hipMemcpyAsync(p.d_items[g], p.items[g].data(), p.items[g].size() * sizeof(GradItem),
-                        hipMemcpyHostToDevice, ctx->stream));
+    for (auto& g : p.groups) {
+      CK(dalloc(&g.d_items, (int64_t)g.items.size()));
+      CK(hipMemcpyAsync(g.d_items, g.items.data(), g.items.size() * sizeof(GradItem), hipMemcpyHostToDevice,
+                        ctx->stream));
     }
   } else {
     p.owns = false;
@@ -300,12 +324,12 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
     int64_t off = 0;
-    for (int g = 0; g < BANN_NGROUPS; ++g) {
-      if (p.items[g].empty()) continue;
-      p.d_items[g] = ctx->d_items_scr + off;
-      CK(hipMemcpyAsync(p.d_items[g], p.items[g].data(), p.items[g].size() * sizeof(GradItem),
-                        hipMemcpyHostToDevice, ctx->stream));
-      off += (int64_t)p.items[g].size();
+    for (auto& g : p.groups) {
+      if (off + (int64_t)g.items.size() > ctx->items_cap) return fail(ctx, BANN_E_STATE, "work-item scratch overflow");
+      g.d_items = ctx->d_items_scr + off;
+      CK(hipMemcpyAsync(g.d_items, g.items.data(), g.items.size() * sizeof(GradItem), hipMemcpyHostToDevice,
+                        ctx->stream));
+      off += (int64_t)g.items.size();
     }
   }
   return BANN_OK;
@@ -313,14 +337,14 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 
 // gradient (partials) of every branch in the plan at the current theta
 static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
-  for (int g = 0; g < BANN_NGROUPS; ++g) {
-    if (p.items[g].empty()) continue;
-    if (g >= BANN_WIDE_GROUP0)
-      launch_fused_grad_wx(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), g - BANN_WIDE_GROUP0,
-                           ctx->wide_bf16 ? 1 : 0, write_pred, ctx->stream);
+  for (const auto& g : p.groups) {
+    const int32_t ni = (int32_t)g.items.size();
+    if (g.kind == 2)
+      launch_fused_grad_wx(ctx->st, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, write_pred, ctx->stream);
+    else if (g.kind == 3)
+      launch_fused_grad_fxl(ctx->st, g.d_items, ni, g.L, g.act, g.nw, g.full, write_pred, ctx->stream);
     else
-      launch_fused_grad(ctx->st, p.d_items[g], (int32_t)p.items[g].size(), p.nwaves[g], g / 15 + 2, (g / 3) % 5,
-                        g % 3 == 1, write_pred, ctx->stream);
+      launch_fused_grad_fx(ctx->st, g.d_items, ni, g.L, g.act, g.full, write_pred, ctx->stream);
   }
   if (!p.generic.empty())
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
@@ -373,7 +397,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
     (void)hipFree(ctx->d_dbg);
   }
   free_plan(ctx->lf);
-  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xpk, ctx->d_xu2, ctx->d_dig, ctx->d_fc, ctx->d_mub,
+  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xu2, ctx->d_dig, ctx->d_fc, ctx->d_mub,
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
@@ -561,7 +585,7 @@ extern "C" int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b) {
   if (!check_branch(ctx, b)) return BANN_E_ARG;
   return ctx->br[b].dev.fused;
 }
-extern "C" const char* bann_fused_kernel_name(void) { return fused_kernel_family(); }
+extern "C" const char* bann_fused_kernel_name(void) { return "k_fused_grad_fx"; }
 
 extern "C" int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled) {
   if (!ctx) return BANN_E_ARG;
@@ -585,32 +609,28 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   const int64_t n = ctx->n;
   ctx->nfrag = (int32_t)((n + 15) / 16);
   const int64_t npad = (int64_t)ctx->nfrag * 16;
-  // row splits of the fused kernel: ~target work items over all branches
+  // kernel path per branch: fx (widths <= 4, <= 8 chunks), fxl (widths <= 4,
+  // 9..64 chunks), wx (one hidden layer up to 32 x 32, m <= 128), else generic
   int64_t total_frags = 0;
   for (auto& h : ctx->br) {
     for (int i = 0; i < h.m; ++i)
       if (h.snp_idx[i] >= ctx->M) return fail(ctx, BANN_E_SHAPE, "marker index out of range");
     BranchDev& d = h.dev;
     d.nchunks = (h.m + BANN_CHUNK - 1) / BANN_CHUNK;
-    bool ok = ctx->fused_enabled && h.L >= 2 && h.L <= 4 && d.nchunks <= BANN_FUSED_MAXCH;
-    for (int l = 0; l < h.L; ++l) ok = ok && h.widths[l] <= BANN_FUSED_MAXW;
-    d.fused = ok ? 1 : 0;
-    // wide branches (one hidden layer up to 32 x 32, m <= 256): the wx kernel
-    if (!ok && ctx->fused_enabled && h.L == 3 && d.nchunks <= BANN_WIDE_MAXCH && h.widths[0] <= BANN_WIDE_MAXW &&
-        h.widths[1] <= BANN_WIDE_MAXW)
+    bool narrow = ctx->fused_enabled && h.L >= 2 && h.L <= 4;
+    for (int l = 0; l < h.L; ++l) narrow = narrow && h.widths[l] <= BANN_FUSED_MAXW;
+    d.fused = 0;
+    if (narrow && d.nchunks <= BANN_FX_MAXCH)
+      d.fused = 1;
+    else if (narrow && d.nchunks <= BANN_FXL_MAXCH)
+      d.fused = 3;
+    else if (ctx->fused_enabled && h.L == 3 && d.nchunks <= BANN_WIDE_MAXCH && h.widths[0] <= BANN_WIDE_MAXW &&
+             h.widths[1] <= BANN_WIDE_MAXW)
       d.fused = 2;
     if (d.fused) total_frags += ctx->nfrag;
   }
-  int64_t target_items = 1024;  // fewer, longer items: -1..2 % (prologue + barrier skew)
-  if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
-  int64_t min_frags = 64;  // >= 16 tiles per work item amortises the per-item prologue/epilogue
-  if (const char* e = getenv("BANN_MIN_FRAGS")) min_frags = std::max<int64_t>(1, atoll(e));
-  const int64_t frags_per_item =
-      std::max<int64_t>(min_frags, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
-  // genotype storage of the fused branches: 2-bit codes when the kernel family
-  // reads them and every genotype is a 2-bit value (0..3), else int8
-  ctx->u2 = false;
-  if (fused_prefers_u2() && total_frags > 0) {
+  // every kernel reads 2-bit genotype codes (.bed semantics: 0, 1, 2; 3 is accepted)
+  {
     int32_t* d_flag = nullptr;
     int32_t flag = 0;
     CK(dalloc(&d_flag, 1));
@@ -620,44 +640,58 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     CK(hipMemcpyAsync(&flag, d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
     dfree(d_flag);
-    ctx->u2 = flag == 0;
+    if (flag) return fail(ctx, BANN_E_ARG, "genotypes must be 2-bit codes in 0..3 (.bed semantics)");
   }
+  int64_t target_items = 1024;  // wx (and fx with BANN_TARGET_ITEMS / BANN_MIN_FRAGS): ~target work items
+  if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
+  int64_t min_frags = 64;  // >= 16 tiles per work item amortises the per-item prologue/epilogue
+  if (const char* e = getenv("BANN_MIN_FRAGS")) min_frags = std::max<int64_t>(1, atoll(e));
+  const int64_t frags_per_item =
+      std::max<int64_t>(min_frags, (total_frags + target_items - 1) / std::max<int64_t>(1, target_items));
   const int64_t ntile = (ctx->nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
-  // Splits of the 4-wide fused (fx) branches: whole rounds of resident
-  // workgroups.  All items of a packed launch are equally long, so a launch
-  // costs ceil(items / slots) rounds of (per-item prologue/epilogue + tiles per
-  // wave); choose the split count minimising that (e.g. 125 branches on one GPU
-  // of an 8-GPU shard: 4 splits = 500 items in one round, where the
-  // 1024-item target gave 9 splits = 1125 items in 3 partly empty rounds).
-  int32_t fx_splits = 0;
-  if (!getenv("BANN_TARGET_ITEMS") && !getenv("BANN_MIN_FRAGS")) {
-    int64_t nfx = 0;
-    for (auto& h : ctx->br) nfx += h.dev.fused == 1 ? 1 : 0;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
-      cus = 256;
-    const int64_t slots = 2 * (int64_t)cus;  // k_fused_grad_fx: two workgroups per CU
-    double best = 0.0;
-    for (int32_t sp = 1; nfx > 0 && sp <= 64 && 4 * sp <= ntile; ++sp) {
-      const int64_t rounds = (nfx * sp + slots - 1) / slots;
-      const int64_t per_wave = (ntile + 4 * sp - 1) / (4 * sp);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+    cus = 256;
+  // Splits: whole rounds of resident workgroups.  All items of a packed launch
+  // are equally long, so a launch costs ceil(items / slots) rounds of (per-item
+  // prologue/epilogue + tiles per wave); choose the split count minimising that
+  // (e.g. 125 fx branches on one GPU of an 8-GPU shard: 4 splits = 500 items in
+  // one round, where a 1024-item target gave 9 splits = 1125 items in 3 partly
+  // empty rounds).  Lower bound: <= BANN_MAX_TILES_PER_WAVE tiles per wave, so
+  // the int32 dW0 digit sums cannot overflow.
+  auto best_splits = [&](int64_t nbr, int64_t slots, int64_t tiles_per_split_wave_div) -> int32_t {
+    const int64_t min_sp = (ntile + tiles_per_split_wave_div * BANN_MAX_TILES_PER_WAVE - 1) /
+                           (tiles_per_split_wave_div * BANN_MAX_TILES_PER_WAVE);
+    int32_t best_sp = (int32_t)std::max<int64_t>(1, min_sp);
+    double best = -1.0;
+    for (int64_t sp = std::max<int64_t>(1, min_sp); nbr > 0 && sp <= std::max<int64_t>(64, min_sp); ++sp) {
+      if (sp > min_sp && tiles_per_split_wave_div * sp > ntile) break;
+      const int64_t rounds = (nbr * sp + slots - 1) / slots;
+      const int64_t per_wave = (ntile + tiles_per_split_wave_div * sp - 1) / (tiles_per_split_wave_div * sp);
       const double cost = (double)rounds * (2.0 + (double)per_wave);  // ~2 tiles of prologue + epilogue
-      if (fx_splits == 0 || cost < best) best = cost, fx_splits = sp;
+      if (best < 0.0 || cost < best) best = cost, best_sp = (int32_t)sp;
     }
+    return best_sp;
+  };
+  const bool env_split = getenv("BANN_TARGET_ITEMS") || getenv("BANN_MIN_FRAGS");
+  int64_t nfx = 0, nfxl[9] = {};
+  for (auto& h : ctx->br) {
+    if (h.dev.fused == 1) ++nfx;
+    if (h.dev.fused == 3) ++nfxl[(h.dev.nchunks + 7) / 8];
   }
-  int64_t x_off = 0, x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
+  const int32_t fx_splits = best_splits(nfx, 2 * (int64_t)cus, 4);  // fx: 2 workgroups of 4 waves per CU, tiles interleaved
+  int32_t fxl_splits[9] = {};
+  for (int nw = 2; nw <= 8; ++nw) {  // fxl: all waves of a workgroup on one tile; LDS- and VGPR-limited residency
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4), 8 / nw));
+    fxl_splits[nw] = best_splits(nfxl[nw], per_cu * cus, 1);
+  }
+  int64_t x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     BranchDev& d = h.dev;
-    if (d.fused == 2 && !(ctx->u2 && fused_u2_layout())) d.fused = 0;  // wx reads the 2-bit tile image only
-    if (d.fused && ctx->u2 && d.nchunks <= 8) {  // the register-staged kernel serves <= 8 chunks
-      d.x_off = x2_off;  // byte offset into the 2-bit buffer: [tile][chunk][64 lanes][16 B]
-      x2_off += ntile * d.nchunks * 1024;
-    } else {
-      d.x_off = x_off;
-      x_off += (int64_t)ctx->nfrag * d.nchunks * 1024;
-    }
+    d.x_off = x2_off;  // byte offset of the branch's 2-bit tile image: [tile][chunk][1 KiB]
+    x2_off += ntile * d.nchunks * 1024;
     d.dig_off = dig_off;
     if (d.fused) dig_off += (int64_t)d.nchunks * 1024 * (d.fused == 2 ? 8 : 1);
     d.p_off = p_off;
@@ -666,8 +700,12 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     mk_off += h.m;
     d.y_off = (int64_t)b * n;
     d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
-    if (d.fused == 1 && fx_splits > 0) d.nsplits = fx_splits;
-    d.nsplits = (int32_t)std::min<int64_t>(d.nsplits, ntile);
+    if (d.fused == 1 && !env_split) d.nsplits = fx_splits;
+    if (d.fused == 3) d.nsplits = fxl_splits[(d.nchunks + 7) / 8];
+    if (d.fused == 1)  // overflow guard also under the env overrides
+      d.nsplits = std::max<int32_t>(d.nsplits, (int32_t)((ntile + 4 * BANN_MAX_TILES_PER_WAVE - 1) /
+                                                         (4 * BANN_MAX_TILES_PER_WAVE)));
+    d.nsplits = (int32_t)std::max<int64_t>(1, std::min<int64_t>(d.nsplits, ntile));
     if (d.fused) items += d.nsplits;
     if (d.fused == 2) d.nsplits *= 4;  // wx: every wave of an item writes its own slab
     max_splits = std::max(max_splits, d.nsplits);
@@ -691,11 +729,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     }
   }
   ctx->max_splits = max_splits;
-  ctx->packed_bytes = x_off + x2_off;
+  ctx->packed_bytes = x2_off;
   ctx->total_p = p_off;
   const int64_t nb = (int64_t)ctx->br.size();
-  CK(dalloc(&ctx->d_xpk, std::max<int64_t>(x_off, 16)));
-  if (x2_off) CK(dalloc(&ctx->d_xu2, x2_off));
+  CK(dalloc(&ctx->d_xu2, x2_off));
   CK(dalloc(&ctx->d_dig, dig_off));
   CK(hipMemsetAsync(ctx->d_dig, 0, (size_t)std::max<int64_t>(dig_off, 1), ctx->stream));
   CK(dalloc(&ctx->d_fc, nb));
@@ -746,14 +783,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
     CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8 && fused_u2_layout())
-      launch_pack_branch_u2t(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
-                             ctx->stream);
-    else if (h.dev.fused && ctx->u2 && h.dev.nchunks <= 8)
-      launch_pack_branch_u2(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
-                            ctx->stream);
-    else
-      launch_pack_branch(ctx->d_g, d_idx, h.m, n, ctx->d_xpk + h.dev.x_off, h.dev.nchunks, ctx->nfrag, ctx->stream);
+    launch_pack_branch_u2t(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
+                           ctx->stream);
     launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, h.m, ctx->d_mub + h.dev.mk_off, ctx->d_sigb + h.dev.mk_off,
                         ctx->stream);
     CK(hipGetLastError());

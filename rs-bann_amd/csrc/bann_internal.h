@@ -5,10 +5,12 @@
 #include <stdint.h>
 
 #define BANN_MAXL 8          // max layers per branch (hidden + summary + output)
-#define BANN_FUSED_MAXW 4    // fused kernel: every layer width <= 4
+#define BANN_FUSED_MAXW 4    // fused kernels (fx, fxl): every layer width <= 4
 #define BANN_WIDE_MAXW 32    // wide fused kernel (wx): one hidden layer, W, S <= 32
 #define BANN_WIDE_MAXCH 2    // wide fused kernel: m_b <= 128
-#define BANN_FUSED_MAXCH 16  // fused kernel: <= 16 marker chunks of 64 (m_b <= 1024)
+#define BANN_FX_MAXCH 8      // fx: <= 8 marker chunks of 64 (m_b <= 512), one wave per tile
+#define BANN_FXL_MAXCH 64    // fxl: <= 64 chunks (m_b <= 4096), one wave per <= 8-chunk block
+#define BANN_MAX_TILES_PER_WAVE 4096  // int32 dW0 digit sums: < 2^31 / (3.9e5 per tile)
 #define BANN_CHUNK 64        // markers per chunk (one 16x16x64 i8 MFMA K-step)
 #define BANN_FRAG 16         // individuals per fragment (MFMA N)
 #define BANN_TILE_FRAGS 4    // fragments per fused-kernel tile (64 individuals)
@@ -32,7 +34,7 @@ struct BranchDev {
   int32_t prior;      // bann_prior
   int32_t P;          // num params
   int32_t nsplits;    // row splits (partial slabs)
-  int32_t fused;      // 1 = fused kernel path (widths <= 4), 2 = wide fused kernel (wx), 0 = generic
+  int32_t fused;      // kernel path: 1 = fx, 3 = fxl (widths <= 4), 2 = wide (wx), 0 = generic
   int32_t widths[BANN_MAXL];  // out width of each layer (last = 1)
   int32_t win[BANN_MAXL];     // in width of each layer (win[0] = m)
   int32_t woff[BANN_MAXL];    // param_vec offset of W_l
@@ -59,8 +61,7 @@ struct FusedConst {
 
 struct DevState {
   const BranchDev* br;    // [nbranch]
-  const int8_t* xpk;      // packed int8 genotypes ([frag][chunk][lane][16 B])
-  const uint8_t* xu2;     // packed 2-bit genotypes ([tile][chunk][lane][4 x u32]), fused branches
+  const uint8_t* xu2;     // 2-bit genotype tile images of every branch ([tile][chunk][1 KiB], kernels_fx.hip)
   const uint8_t* dig;     // digits
   FusedConst* fc;         // [nbranch]
   const float* mu;        // gathered per-branch marker means  [sum m]
@@ -91,7 +92,6 @@ struct DevState {
   int32_t max_splits;
   int32_t lint;           // trajectory length L (for the trace stride)
   float max_dh;
-  int32_t u2;             // fused branches read xu2 (2-bit) instead of xpk
   unsigned long long* dbg;  // diagnostic phase stamps (BANN_STAMPS=1 with a BANN_ABLATE=16 build), else null
 };
 
@@ -100,19 +100,11 @@ void launch_synthetic_genotypes(int8_t* g, float* mu, float* sigma, int64_t n, i
                                 hipStream_t s);
 void launch_decode_bed(const uint8_t* payload, int8_t* g, int64_t n, int64_t M, hipStream_t s);
 void launch_col_stats(const int8_t* g, float* mu, float* sigma, int64_t n, int64_t M, hipStream_t s);
-void launch_pack_branch(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* dst, int32_t nchunks,
-                        int32_t nfrag, hipStream_t s);
 void launch_unpack_markers(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* out,
                            hipStream_t s);
 void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp_idx, int32_t m, float* mu_b,
                          float* sig_b, hipStream_t s);
 
-void launch_fused_grad(const DevState& st, const GradItem* items, int32_t nitems, int32_t nwaves, int32_t L,
-                       int32_t act, int full8, int write_pred, hipStream_t s);
-// fused launch groups: ((L - 2) * 5 + activation) * 3 + (nchunks < 8 ? 0 : nchunks == 8 ? 1 : 2), L in [2, 4]
-// + 5 wide groups (one per activation): BANN_WIDE_GROUP0 + activation
-#define BANN_WIDE_GROUP0 45
-#define BANN_NGROUPS 50
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
@@ -120,16 +112,14 @@ void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int3
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
-const char* fused_kernel_family();
-int fused_prefers_u2();
-int fused_u2_layout();              // 1: fx tile-row image (launch_pack_branch_u2t), 0: rx image             // the fused variant reads 2-bit genotypes unless BANN_GENO_FORMAT=i8
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
-void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
-                           int32_t nchunks, int32_t ntile, hipStream_t s);  // kernel used for <= 8 chunks (BANN_FUSED_VARIANT)
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
                           int write_pred, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, hipStream_t s);
+void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
+                           int32_t nw, int full, int write_pred, hipStream_t s);
+int fxl_lds_bytes(int nw, int nl);
 void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
                             int32_t nchunks, int32_t ntile, hipStream_t s);
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,

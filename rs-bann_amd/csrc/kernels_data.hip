@@ -155,77 +155,6 @@ void launch_col_stats(const int8_t* g, float* mu, float* sigma, int64_t n, int64
   hipLaunchKernelGGL(k_col_stats, dim3((unsigned)M), dim3(256), 0, s, g, mu, sigma, n);
 }
 
-// ---------------------------------------------------------------------------
-// pack one branch: gather its markers (any index list; overlapping groups are
-// simply copied) into the fragment-major layout.  Padding (individuals >= n,
-// markers >= m) is zero.  One thread per 16-byte lane slot.
-// ---------------------------------------------------------------------------
-__global__ void k_pack(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,
-                       int8_t* __restrict__ dst, int32_t nchunks, int32_t nfrag) {
-  const int64_t slots = (int64_t)nfrag * nchunks * 64;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < slots;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(t & 63);
-    const int64_t fc = t >> 6;
-    const int c = (int)(fc % nchunks);
-    const int64_t f = fc / nchunks;
-    const int64_t row = 16 * f + (lane & 15);
-    const int snp0 = 64 * c + 16 * (lane >> 4);
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (row < n) {
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        const int s = snp0 + jj;
-        uint32_t v = 0;
-        if (s < m) v = (uint8_t)g[(int64_t)idx[s] * n + row];
-        w[jj >> 2] |= v << (8 * (jj & 3));
-      }
-    }
-    uint4* d = reinterpret_cast<uint4*>(dst + t * 16);
-    *d = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-}
-
-void launch_pack_branch(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* dst, int32_t nchunks,
-                        int32_t nfrag, hipStream_t s) {
-  const int64_t slots = (int64_t)nfrag * nchunks * 64;
-  const int64_t blocks = (slots + 255) / 256;
-  hipLaunchKernelGGL(k_pack, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, g, snp_idx, m, n,
-                     dst, nchunks, nfrag);
-}
-
-// 2-bit packing for the register-staged fused kernel: per (tile of 4 fragments,
-// chunk, lane) four u32 words, word q = fragment q of the tile; genotype
-// j = 4k + b of the lane's 16 (individual 16f + (lane & 15), marker
-// 64c + 16(lane >> 4) + j) at bits 8b + 2k, so (w >> 2k) & 0x03030303 is the
-// int8 B-operand word k.  Padding (markers >= m, individuals >= n) is 0.
-__global__ void k_pack_u2(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,
-                          uint8_t* __restrict__ dst, int32_t nchunks, int32_t ntile) {
-  const int64_t slots = (int64_t)ntile * nchunks * 64;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < slots;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(t & 63);
-    const int64_t tc = t >> 6;
-    const int c = (int)(tc % nchunks);
-    const int64_t tile = tc / nchunks;
-    const int snp0 = 64 * c + 16 * (lane >> 4);
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t row = 16 * (4 * tile + q) + (lane & 15);
-      if (row >= n) continue;
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        const int s = snp0 + jj;
-        uint32_t v = 0;
-        if (s < m) v = (uint32_t)g[(int64_t)idx[s] * n + row] & 3u;
-        w[q] |= v << (8 * (jj & 3) + 2 * (jj >> 2));
-      }
-    }
-    *reinterpret_cast<uint4*>(dst + t * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-}
-
 __global__ void k_check_2bit(const int8_t* __restrict__ g, int64_t count, int32_t* __restrict__ flag) {
   int bad = 0;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (int64_t)gridDim.x * blockDim.x)
@@ -238,14 +167,6 @@ void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_
   const int64_t blocks = (count + 255) / 256;
   hipLaunchKernelGGL(k_check_2bit, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, g, count,
                      flag);
-}
-
-void launch_pack_branch_u2(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
-                           int32_t nchunks, int32_t ntile, hipStream_t s) {
-  const int64_t slots = (int64_t)ntile * nchunks * 64;
-  const int64_t blocks = (slots + 255) / 256;
-  hipLaunchKernelGGL(k_pack_u2, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, g, snp_idx, m,
-                     n, dst, nchunks, ntile);
 }
 
 __global__ void k_unpack(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,

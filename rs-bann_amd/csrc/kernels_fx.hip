@@ -661,6 +661,473 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
   }
 }
 
+// ===========================================================================
+// "fxl": the fx scheme for branches of 9 .. 64 marker chunks (m_b <= 4096, e.g.
+// BASELINE config C2's 2 000-SNP branches).
+//
+// An fx wave keeps the int32 dW0 digit sums of ALL its branch's markers in
+// registers (128 VGPRs at 8 chunks), so fx stops at 512 markers.  Here a
+// workgroup of NW = ceil(chunks / 8) waves processes ONE 64-individual tile at a
+// time and wave w owns a fixed block of <= 8 chunks for the whole item:
+//   * forward: each wave's partial Z0 over its block (exact int32, one f32
+//     conversion), published through LDS (double-buffered, one barrier per
+//     tile) and summed in a fixed wave order -- identical in every wave;
+//   * head + delta0 digits: in every wave (the same values, no second barrier);
+//   * backward: dW0 digit sums of the wave's own block, in registers across all
+//     tiles of the item, written straight to the partial slab at the end.
+// The genotype block of the next tile streams into the wave's second LDS slot
+// during the forward (LDS-DMA, counted vmcnt), as in fx.  The LDS holds the two
+// tile slots, the delta0 digit image and the Z0 exchange (19 KiB per wave: two
+// 4-wave workgroups per CU), so the W0/sigma digit operand is read from L2 into
+// registers two chunks ahead with counted loads instead of an LDS image.
+// ===========================================================================
+#define FXL_MAXW 8
+
+// one global_load_dwordx4 outside the compiler's wait model (counted by hand)
+__device__ __forceinline__ v4i ld_counted(const char* p) {
+  v4i d;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
+  return d;
+}
+// wait until at most k vector-memory ops are outstanding, and only then let d be used
+__device__ __forceinline__ void vm_wait_tie(int k, v4i& d) {
+  switch (k) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" : "+v"(d)::"memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" : "+v"(d)::"memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" : "+v"(d)::"memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(3)" : "+v"(d)::"memory"); break;
+  }
+}
+
+int fxl_lds_bytes(int nw, int nl) {
+  const int ns = 8 + (nl - 2) * 20;
+  return nw * (2 * FX_SLOT + 4 * FX_DROW + 2 * 64 * 16) + 2 * 64 * 4 + nl * 20 * 4 + ns * 4;
+}
+
+template <int NL, int ACT, int FULL>
+__global__ void __launch_bounds__(64 * FXL_MAXW, 1)
+    k_fused_grad_fxl(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  // Counted digit loads only where the kernel fits in 256 VGPRs without spills
+  // (every wave 8 chunks, <= 3 layers: C2's shape): a spill of a register whose
+  // load is still in flight would store garbage.  Elsewhere the digit loads are
+  // ordinary loads under the compiler's own (conservative) waits.
+  constexpr bool CNT = FULL && NL <= 3;
+  constexpr int NH = NL - 1;
+  constexpr int NS = 8 + (NH - 1) * 20;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int NW = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
+  char* const s_x = lds;                                                    // [NW][2][FX_SLOT]
+  char* const s_dig = s_x + NW * 2 * FX_SLOT;                               // [NW][4 * FX_DROW]
+  v4f* const s_xch = reinterpret_cast<v4f*>(s_dig + NW * 4 * FX_DROW);      // [2][NW][64]
+  float* const s_y = reinterpret_cast<float*>(s_xch + 2 * NW * 64);         // [2][64]
+  float* const s_hw = s_y + 128;                                            // [NL][20]
+  float* const s_hs = s_hw + NL * 20;                                       // [NS]
+
+  const GradItem it = items[blockIdx.x];
+  const int b = it.branch;
+  const BranchDev& bd = st.br[b];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = bd.nchunks;
+  const int cpw = FULL ? 8 : (nch + NW - 1) / NW;
+  const int c0 = wave * cpw;
+  const int cw = FULL ? 8 : (nch - c0 < cpw ? nch - c0 : cpw);  // >= 1 (NW = ceil(nch / 8))
+  const int64_t n = st.n;
+  const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
+
+  const float* th = st.theta + bd.p_off;
+  for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (r < 16) {
+      const int j = r >> 2, k = r & 3;
+      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+    } else {
+      const int k = r - 16;
+      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+    }
+    s_hw[t] = v;
+  }
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
+  float zscale = st.fc[b].scale[g];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(zscale));
+  __syncthreads();
+
+  const int gsw = g & 1;
+  const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
+  const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
+  const int pe = i16, po = (i16 + 8) & 15;
+  const uint32_t boe = (uint32_t)(pe * 16 + 4 * (2 * ((g >> 1) ^ (pe >> 3)) + (g & 1)));
+  const uint32_t boo = (uint32_t)(po * 16 + 4 * (2 * ((g >> 1) ^ (po >> 3)) + (g & 1)));
+  const int iota = 4 * i16 + g;
+  char* const sd = s_dig + wave * 4 * FX_DROW;
+  char* const sd_w = sd + (i16 >> 2) * FX_DROW + (4 * g + (i16 & 3)) * 16;
+  const char* const sd_r = sd + g * FX_DROW + tq * 16 + 8 * tp;
+  const float* ybr = st.y + bd.y_off;
+  float* predb = st.pred + bd.y_off;
+  const int64_t tile_bytes = (int64_t)nch * 1024;
+  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + (int64_t)c0 * 1024 + lane * 16;
+  const char* dsrc = reinterpret_cast<const char*>(st.dig) + bd.dig_off + (int64_t)c0 * 1024 + lane * 16;
+  char* const xslot0 = s_x + wave * 2 * FX_SLOT;
+
+  auto issue_chunk = [&](int tt, int sl, int c) {
+    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, xslot0 + sl * FX_SLOT + c * 1024);
+  };
+  auto issue_y = [&](int tt, int sl) {  // wave 0 streams the tile's targets for every wave
+    if (wave != 0) return;
+    const int64_t row = 64 * (int64_t)tt + iota;
+    glds4(ybr + (row < n ? row : n - 1), s_y + sl * 64);
+  };
+
+  v4i acc[32];
+#pragma unroll
+  for (int u = 0; u < 32; ++u) acc[u] = v4i{0, 0, 0, 0};
+  int R[4] = {0, 0, 0, 0};
+  double rss = 0.0;
+  float db[NH][4], dWo[4];
+  float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    dWo[k] = 0.f;
+#pragma unroll
+    for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+    for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+  }
+
+  int tt = tb, sl = 0, xb = 0;
+  if (tt < te) {
+    for (int c = 0; c < cw; ++c) issue_chunk(tt, 0, c);
+    issue_y(tt, 0);
+  }
+  auto ldig = [&](int off) -> v4i {
+    if constexpr (CNT) return ld_counted(dsrc + off);
+    return *reinterpret_cast<const v4i*>(dsrc + off);
+  };
+  v4i Dn0 = ldig(0), Dn1 = Dn0;
+  if (FULL || cw > 1) Dn1 = ldig(1024);
+  for (; tt < te; ++tt, sl ^= 1, xb ^= 1) {
+    const bool more = tt + 1 < te;
+    // this tile's genotype block (and targets) have landed; the two digit loads may fly
+    vm_wait((FULL || cw > 1) ? 2 : 1);
+    const char* xs = xslot0 + sl * FX_SLOT;
+
+    // ---- forward: partial Z0 over this wave's block ----
+    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+    {
+      v4i Dg[8];
+      Dg[0] = Dn0;
+      Dg[1] = Dn1;
+      v4u Xc = (v4u)lds_tr8_pair(xs + fo0, xs + fo1);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (!FULL && c >= cw) continue;
+        v4u Xn = Xc;
+        if (c + 1 < 8 && (FULL || c + 1 < cw))
+          Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
+        if constexpr (CNT) {
+          // loads younger than digit load c (issue order below: D(c+2) then
+          // piece c per chunk, the pieces issued on every tile so the count is a
+          // compile-time constant -- a runtime count would need a branch, and the
+          // compiler copies the tied register ahead of the wait on one side)
+          constexpr int young_c[8] = {1, 2, 3, 3, 3, 3, 3, 2};
+          vm_wait_tie(young_c[c], Dg[c]);
+        }
+        if (c + 2 < 8 && (FULL || c + 2 < cw)) Dg[c + 2] = ldig((c + 2) * 1024);
+        if (more)
+          issue_chunk(tt + 1, sl ^ 1, c);
+        else if (CNT)  // last tile: a harmless L2-resident DMA keeps the counts fixed
+          glds16(dsrc + c * 1024, xslot0 + (sl ^ 1) * FX_SLOT + c * 1024);
+        const v4i B0 = (v4i)(Xc & 0x03030303u);
+        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
+        const v4i B2 = (v4i)(Xc & 0x30303030u);
+        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
+        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B0, facc[0], 0, 0, 0);
+        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B1, facc[1], 0, 0, 0);
+        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B2, facc[2], 0, 0, 0);
+        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B3, facc[3], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        Xc = Xn;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
+    swap32(z0, z2);
+    swap32(z1, z3);
+    swap16(z0, z1);
+    swap16(z2, z3);
+    // ---- Z0 exchange: every wave sums the NW partials in wave order ----
+    v4f* xw = s_xch + (xb * NW) * 64;
+    lds_st_v4f(xw + wave * 64 + lane, v4f{z0, z1, z2, z3});
+    LDS_BARRIER();
+    {
+      v4f zs = xw[lane];
+      for (int w = 1; w < NW; ++w) zs += xw[w * 64 + lane];
+      z0 = zs[0];
+      z1 = zs[1];
+      z2 = zs[2];
+      z3 = zs[3];
+    }
+
+    // ---- head: one individual per lane (every wave, identical values) ----
+    const int64_t row = 64 * (int64_t)tt + iota;
+    const bool valid = row < n;
+    const float yv = s_y[sl * 64 + lane];
+    if (more) issue_y(tt + 1, sl ^ 1);
+    float d[4];
+    {
+      float Wh[NL][4][4], Bh[NH][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l * 20 + 4 * j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Wh[l][j][k] = r4[k];
+          }
+        }
+        if (l < NH) {
+          const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l * 20 + 16]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
+        }
+      }
+      float z[NH][4], a[NH][4];
+      z[0][0] = z0 + Bh[0][0];
+      z[0][1] = z1 + Bh[0][1];
+      z[0][2] = z2 + Bh[0][2];
+      z[0][3] = z3 + Bh[0][3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[0][k] = act_h_t<ACT>(z[0][k]);
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float s = Bh[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s = fmaf(a[l - 1][j], Wh[l][j][k], s);
+          z[l][k] = s;
+          a[l][k] = act_h_t<ACT>(s);
+        }
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], Wh[NL - 1][j][0], out);
+      const float e = valid ? out - yv : 0.f;
+      if (write_pred && valid && wave == 0) predb[row] = out;
+      rss += (double)e * (double)e;
+      float err[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+        err[j] = e * Wh[NL - 1][j][0];
+      }
+#pragma unroll
+      for (int l = NH - 1; l >= 0; --l) {
+        float dl[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dl[k] = act_dh_t<ACT>(z[l][k], a[l][k]) * err[k];
+          db[l][k] += dl[k];
+        }
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float sj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dW[l - 1][j][k] = fmaf(a[l - 1][j], dl[k], dW[l - 1][j][k]);
+              sj = fmaf(dl[k], Wh[l][j][k], sj);
+            }
+            err[j] = sj;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[k] = dl[k];
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- delta0 -> signed digits at the running per-column scale (as fx) ----
+    int dl[4] = {0, 0, 0, 0};
+    bool grow = false;
+    {
+      bool need = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ek = (int)((fbits(d[k]) >> 23) & 0xFFu);
+        need = need || __builtin_amdgcn_ballot_w64(ek > (R[k] ? R[k] : 5)) != 0;
+      }
+      if (need) {
+        const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+        const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+        const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (E[k] >= 6 && (R[k] == 0 || E[k] > R[k])) {
+            if (R[k] != 0) {
+              dl[k] = E[k] + 2 - R[k];
+              grow = true;
+            }
+            R[k] = E[k] + 2;
+          }
+        }
+      }
+    }
+    if (grow) {
+      const int sh = g == 0 ? dl[0] : g == 1 ? dl[1] : g == 2 ? dl[2] : dl[3];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (FULL || u < 4 * cw) acc[u] = shr_digits(acc[u], sh);
+    }
+    v4u w;
+    const int kslot_sh = g == 1 ? 2 : g == 2 ? 4 : 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - kslot_sh - (R[k] ? R[k] : 255));
+    *reinterpret_cast<v4u*>(sd_w) = w;
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+
+    // ---- backward: dW0 digit sums of this wave's block += G^T delta0 ----
+    const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
+    {
+      constexpr int PD = 8;
+      uint32_t wq[PD];
+#pragma unroll
+      for (int u = 0; u < PD; ++u)
+        wq[u] = (FULL || u < 4 * cw) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        if (!FULL && u >= 4 * cw) continue;
+        const uint32_t wv = wq[u % PD];
+        if (u + PD < 32 && (FULL || u + PD < 4 * cw))
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
+                           (int)((wv >> 6) & 0x03030303u)};
+        acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // the next tile's first two digit operands
+    if (more) {
+      Dn0 = ldig(0);
+      if (FULL || cw > 1) Dn1 = ldig(1024);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- epilogue ----
+  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+  float db0[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) db0[k] = wave_sum(db[0][k]);
+  if (wave == 0) {  // head statistics (identical in every wave)
+    const double rs = wave_sum_d(rss);
+    float hs[NS];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hs[k] = db0[k];
+      hs[4 + k] = wave_sum(dWo[k]);
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hs[8 + (l - 1) * 20 + k] = wave_sum(db[l][k]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hs[8 + (l - 1) * 20 + 4 + 4 * j + k] = wave_sum(dW[l - 1][j][k]);
+      }
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q) s_hs[q] = hs[q];
+      st.rss_part[(int64_t)b * st.max_splits + it.split] = rs;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < NS) {
+      const float v = s_hs[lane];
+      const int q = lane;
+      if (q < 4) {
+        if (q < bd.widths[0]) part[bd.boff[0] + q] = v;
+      } else if (q < 8) {
+        const int j = q - 4;
+        if (j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+      } else {
+        const int l = 1 + (q - 8) / 20, r = (q - 8) % 20;
+        if (r < 4) {
+          if (r < bd.widths[l]) part[bd.boff[l] + r] = v;
+        } else {
+          const int j = (r - 4) >> 2, k = (r - 4) & 3;
+          if (j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = v;
+        }
+      }
+    }
+  }
+  {  // this wave's markers: dW0 = (G^T delta0 - mu sum delta0) / sigma
+    const int Rl = g == 0 ? R[0] : g == 1 ? R[1] : g == 2 ? R[2] : R[3];
+    const float dbc = g == 0 ? db0[0] : g == 1 ? db0[1] : g == 2 ? db0[2] : db0[3];
+    const int m = bd.m;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      if (!FULL && u >= 4 * cw) continue;
+      const int mk = 16 * (4 * c0 + u) + i16;
+      if (mk < m && g < bd.widths[0]) {
+        const float s = Rl ? __builtin_amdgcn_ldexpf(comb4_exact(acc[u]), Rl - 153) : 0.f;
+        const float mu = st.mu[bd.mk_off + mk], sg = st.sigma[bd.mk_off + mk];
+        part[bd.woff[0] + g * m + mk] = sg > 0.f ? (s - mu * dbc) / sg : 0.f;
+      }
+    }
+  }
+}
+
+template <int NL, int FULL>
+static void launch_fxl_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nw, int wp,
+                          hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * nw);
+  const size_t shm = (size_t)fxl_lds_bytes(nw, NL);
+#define FXL_GO(A)                                                                                      \
+  do {                                                                                                 \
+    static bool attr_ = false;                                                                         \
+    if (!attr_) {                                                                                      \
+      (void)hipFuncSetAttribute((const void*)k_fused_grad_fxl<NL, A, FULL>,                            \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, fxl_lds_bytes(FXL_MAXW, 4)); \
+      attr_ = true;                                                                                    \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_fused_grad_fxl<NL, A, FULL>), grid, block, shm, s, st, items, wp);           \
+  } while (0)
+  switch (act) {
+    case 0: FXL_GO(0); break;
+    case 1: FXL_GO(1); break;
+    case 2: FXL_GO(2); break;
+    case 3: FXL_GO(3); break;
+    default: FXL_GO(4); break;
+  }
+#undef FXL_GO
+}
+
+// nw waves per workgroup (= ceil(chunks / 8) of every branch of the launch);
+// full: every branch has exactly 8 * nw chunks
+void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
+                           int32_t nw, int full, int write_pred, hipStream_t s) {
+  if (nitems <= 0 || nw < 1 || nw > FXL_MAXW) return;
+  switch (L * 2 + (full ? 1 : 0)) {
+    case 4: launch_fxl_nl<2, 0>(st, items, nitems, act, nw, write_pred, s); break;
+    case 5: launch_fxl_nl<2, 1>(st, items, nitems, act, nw, write_pred, s); break;
+    case 6: launch_fxl_nl<3, 0>(st, items, nitems, act, nw, write_pred, s); break;
+    case 7: launch_fxl_nl<3, 1>(st, items, nitems, act, nw, write_pred, s); break;
+    case 8: launch_fxl_nl<4, 0>(st, items, nitems, act, nw, write_pred, s); break;
+    case 9: launch_fxl_nl<4, 1>(st, items, nitems, act, nw, write_pred, s); break;
+    default: break;
+  }
+}
+
 // ---- "u2t" tile-row genotype image (see the header comment) ----
 __global__ void k_pack_u2t(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,
                            uint8_t* __restrict__ dst, int32_t nchunks, int32_t ntile) {

@@ -83,6 +83,14 @@ CONFIGS = [
     dict(n=257, m=40, widths=[32, 7, 1], act="leaky_relu", prior="lasso_base"),
     dict(n=100, m=64, widths=[12, 32, 1], act="identity", prior="std_normal"),
     dict(n=65, m=1, widths=[6, 6, 1], act="tanh", prior="ridge_ard"),
+    # fxl (widths <= 4, 512 < m <= 4096: one wave per 512-marker block): C2's
+    # 2 000-SNP branch at n = 10 000, full blocks, ragged blocks, 2 and 4 layers
+    dict(n=10000, m=2000, widths=[4, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=1500, m=4096, widths=[4, 4, 1], act="relu", prior="lasso_ard"),
+    dict(n=999, m=4000, widths=[3, 4, 1], act="silu", prior="ridge_base"),
+    dict(n=300, m=577, widths=[4, 1], act="leaky_relu", prior="lasso_base"),
+    dict(n=640, m=1536, widths=[2, 3, 4, 1], act="tanh", prior="ridge_ard"),
+    dict(n=129, m=3000, widths=[4, 2, 1], act="identity", prior="std_normal"),
 ]
 
 
@@ -91,8 +99,10 @@ def expected_path(cfg, fused):
     w, m = cfg["widths"], cfg["m"]
     if not fused:
         return "generic"
-    if max(w) <= 4 and m <= 1024 and len(w) <= 4:
+    if max(w) <= 4 and m <= 512 and len(w) <= 4:
         return "fused"
+    if max(w) <= 4 and m <= 4096 and len(w) <= 4:
+        return "fused_large"
     if len(w) == 3 and max(w) <= 32 and m <= 128:
         return "wide"
     return "generic"
@@ -235,6 +245,52 @@ def test_hmc_step_parity(Ctx, prior, fused, widths):
     final = ctx.get_params(0)
     assert norm_rel(final, O.param_vec(ob_.weights, ob_.biases)) < 1e-5
     assert res["uturn"][0] == out["u_turn_step"]
+    ctx.close()
+
+
+def test_c2_shape_hmc_and_packing(Ctx):
+    """BASELINE config C2's branch shape (2 000 SNPs, W = S = 4, n = 10 000) on the
+    fxl kernel: an HMC trajectory with injected draws matches the oracle, and a
+    packed launch over fxl branches of 2, 4 and 8 wave blocks plus an fx branch
+    gives every branch's oracle gradient; gradients are bitwise reproducible."""
+    rng = np.random.default_rng(23)
+    n, L = 10000, 5
+    shapes = [(2000, [4, 4, 1]), (900, [4, 4, 1]), (4096, [2, 4, 1]), (300, [4, 4, 1])]
+    M = sum(m for m, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w in shapes:
+        br = f32_branch(O.random_branch(rng, m, w))
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32), branch=br, y=np.zeros(n)))
+        off += m
+    ctx = build_context(Ctx, g, specs)
+    assert [ctx.kernel_path(b) for b in range(4)] == ["fused_large"] * 3 + ["fused"]
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    for b, s in enumerate(specs):
+        s["y"] = (O.predict(s["branch"], Xs[b]) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+        ctx.set_target(b, s["y"])
+    for b, s in enumerate(specs):
+        grad, rss = ctx.log_density_gradient(b)
+        ogw, ogb, orss = O.log_density_gradient(s["branch"], Xs[b], s["y"])
+        assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL, b
+        assert scalar_close(rss, orss), (b, rss, orss)
+        grad2, _ = ctx.log_density_gradient(b)
+        assert np.array_equal(grad, grad2)
+    br = specs[0]["branch"]
+    ew, eb = O.izmailov_step_sizes(br, 0.5, L)
+    eps = O.param_vec(ew, eb).astype(np.float32)
+    p0 = rng.normal(size=br.num_params).astype(np.float32)
+    res = ctx.hmc_step([0], L, 10.0, eps=eps, momentum=p0, u=[0.5])
+    ow, ob = O.load_param_vec(eps.astype(np.float64), 2000, br.layer_widths)
+    pw, pb = O.load_param_vec(p0.astype(np.float64), 2000, br.layer_widths)
+    ob_ = br.copy()
+    out = O.hmc_step(ob_, Xs[0], specs[0]["y"], ow, ob, pw, pb, L, 10.0, 0.5)
+    assert res["status"][0] == out["status"]
+    tr = np.asarray(out["trace"])
+    gt = res["trace"][0][: tr.size]
+    assert np.all(np.abs(gt - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (gt, tr)
+    assert norm_rel(ctx.get_params(0), O.param_vec(ob_.weights, ob_.biases)) < 1e-5
     ctx.close()
 
 
