@@ -41,6 +41,7 @@ struct LaunchGroup {
 
 struct Plan {
   std::vector<int32_t> all, generic;
+  int32_t n_small = 0, n_large = 0;  // update kernels: d_all[nb .. nb+n_small) small, then n_large large
   std::vector<LaunchGroup> groups;
   int32_t max_p_generic = 0, max_p = 0;
   int32_t* d_all = nullptr;
@@ -263,6 +264,13 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
     seen[b] = 1;
   }
   p.all.assign(branches, branches + nb);
+  std::vector<int32_t> lists(p.all);
+  for (int i = 0; i < nb; ++i)
+    if (!update_is_large(ctx->br[branches[i]].dev)) lists.push_back(branches[i]);
+  p.n_small = (int32_t)lists.size() - nb;
+  for (int i = 0; i < nb; ++i)
+    if (update_is_large(ctx->br[branches[i]].dev)) lists.push_back(branches[i]);
+  p.n_large = nb - p.n_small;
   const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
   for (int i = 0; i < nb; ++i) {
     const int b = branches[i];
@@ -304,9 +312,9 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
   }
   if (persistent) {
     p.owns = true;
-    CK(dalloc(&p.d_all, nb));
+    CK(dalloc(&p.d_all, 2 * nb));
     CK(dalloc(&p.d_gen, (int64_t)p.generic.size()));
-    CK(hipMemcpyAsync(p.d_all, p.all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     if (!p.generic.empty())
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
@@ -319,7 +327,7 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
     p.owns = false;
     p.d_all = ctx->d_list_scr;
     p.d_gen = ctx->d_gen_scr;
-    CK(hipMemcpyAsync(p.d_all, p.all.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     if (!p.generic.empty())
       CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
@@ -350,6 +358,13 @@ static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
     launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
   CK(hipGetLastError());
   return BANN_OK;
+}
+
+// the fused leapfrog update of every branch in the plan (small and large kernels)
+static void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step) {
+  const int32_t nb = (int32_t)p.all.size();
+  launch_update(ctx->st, p.d_all + nb, p.n_small, mode, step, ctx->stream, 0);
+  launch_update(ctx->st, p.d_all + nb + p.n_small, p.n_large, mode, step, ctx->stream, 1);
 }
 
 static int ensure_htrace(bann_ctx* ctx, int32_t L) {
@@ -768,7 +783,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_rss, nb));
   CK(dalloc(&ctx->d_status, nb));
   CK(dalloc(&ctx->d_uturn, nb));
-  CK(dalloc(&ctx->d_list_scr, nb));
+  CK(dalloc(&ctx->d_list_scr, 2 * nb));
   CK(dalloc(&ctx->d_gen_scr, nb));
   CK(dalloc(&ctx->d_items_scr, items));
   ctx->items_cap = items;
@@ -901,7 +916,7 @@ static int eval_branch(bann_ctx* ctx, int32_t b, int write_pred) {
   if (rc) return rc;
   rc = run_grad(ctx, p, write_pred);
   if (rc) return rc;
-  launch_update(ctx->st, p.d_all, 1, MODE_GRAD, 0, ctx->stream);
+  run_update(ctx, p, MODE_GRAD, 0);
   CK(hipGetLastError());
   return BANN_OK;
 }
@@ -1028,12 +1043,22 @@ static int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, i
     launch_sample_momentum(ctx->st, p.d_all, (int32_t)p.all.size(), p.max_p, seed, ctx->stream);
     CK(hipGetLastError());
   }
-  std::vector<float> uu(ctx->br.size(), 0.f);
-  std::uniform_real_distribution<float> U(0.f, 1.f);
-  for (size_t i = 0; i < p.all.size(); ++i) uu[p.all[i]] = u ? u[i] : U(rng);
-  CK(hipMemcpyAsync(ctx->d_u, uu.data(), uu.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  bool host_data = momentum || (!device_eps);
+  if (u) {  // injected acceptance uniforms (parity runs)
+    std::vector<float> uu(ctx->br.size(), 0.f);
+    for (size_t i = 0; i < p.all.size(); ++i) uu[p.all[i]] = u[i];
+    CK(hipMemcpyAsync(ctx->d_u, uu.data(), uu.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    host_data = true;
+    CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));  // uu goes out of scope
+    return BANN_OK;
+  }
+  // acceptance uniforms u ~ U(0,1) per branch (branch_sampler.rs:546-548) on the device
+  launch_uniforms(ctx->st, p.d_all, (int32_t)p.all.size(), seed, ctx->stream);
   CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
-  CK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
+  // device-only trajectory start (leapfrog sessions): no host round trip; host
+  // vectors (random / injected step sizes, injected momenta) must outlive their copies
+  if (host_data) CK(hipStreamSynchronize(ctx->stream));
   return BANN_OK;
 }
 
@@ -1055,7 +1080,7 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   rc = run_grad(ctx, p, L == 0 ? 1 : 0);
   if (rc) return rc;
   if (L == 0) {  // empty leapfrog loop: accept_or_reject at the initial state accepts
-    launch_update(ctx->st, p.d_all, nb, MODE_GRAD, 0, ctx->stream);
+    run_update(ctx, p, MODE_GRAD, 0);
     CK(hipGetLastError());
     CK(hipStreamSynchronize(ctx->stream));
     for (int i = 0; i < nb; ++i) {
@@ -1067,11 +1092,11 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
         CK(hipMemcpy(log_density_out + i, ctx->d_ld + branches[i], sizeof(double), hipMemcpyDeviceToHost));
     return BANN_OK;
   }
-  launch_update(ctx->st, p.d_all, nb, MODE_INIT, 0, ctx->stream);
+  run_update(ctx, p, MODE_INIT, 0);
   for (int k = 1; k <= L; ++k) {
     rc = run_grad(ctx, p, k == L ? 1 : 0);
     if (rc) return rc;
-    launch_update(ctx->st, p.d_all, nb, k < L ? MODE_STEP : MODE_LAST, k, ctx->stream);
+    run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
   }
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
@@ -1104,7 +1129,7 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
   rc = run_grad(ctx, ctx->lf, 1);
   if (rc) return rc;
   launch_snapshot_pred(ctx->st, ctx->lf.d_all, nb, ctx->stream);
-  launch_update(ctx->st, ctx->lf.d_all, nb, MODE_INIT, 0, ctx->stream);
+  run_update(ctx, ctx->lf, MODE_INIT, 0);
   CK(hipGetLastError());
   ctx->lf_active = true;
   ctx->lf_L = L;
@@ -1120,7 +1145,7 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
     const int step = ++ctx->lf_step;
     int rc = run_grad(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0);
     if (rc) return rc;
-    launch_update(ctx->st, ctx->lf.d_all, nb, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step, ctx->stream);
+    run_update(ctx, ctx->lf, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
   }
   CK(hipGetLastError());
   return BANN_OK;
@@ -1189,7 +1214,7 @@ extern "C" int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms
     if (rc) return rc;
   }
   CK(hipEventRecord(e1, ctx->stream));
-  for (int i = 0; i < iters; ++i) launch_update(ctx->st, ctx->lf.d_all, nb, MODE_PROFILE, 1, ctx->stream);
+  for (int i = 0; i < iters; ++i) run_update(ctx, ctx->lf, MODE_PROFILE, 1);
   CK(hipEventRecord(e2, ctx->stream));
   CK(hipEventSynchronize(e2));
   float t01 = 0.f, t12 = 0.f;

@@ -108,10 +108,12 @@ void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp
 void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
                          hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
-                   hipStream_t s);
+                   hipStream_t s, int large);
+bool update_is_large(const BranchDev& d);  // served by the 1024-thread update kernel
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
+void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
                           int write_pred, hipStream_t s);

@@ -19,40 +19,16 @@
 #include "bann_internal.h"
 #include "rng.h"
 
-#define UPD_THREADS 256
-
-__device__ double block_sum(double v, double* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  double t = 0.0;
-  for (int k = 0; k < UPD_THREADS / 64; ++k) t += red[k];
-  return t;
-}
-
-__device__ float block_max(float v, float* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  float t = red[0];
-  for (int k = 1; k < UPD_THREADS / 64; ++k) t = fmaxf(t, red[k]);
-  return t;
-}
+#define UPD_THREADS 256   // small branches (P <= 2048, m <= 512: C3 / C4)
+#define UPD_THREADS_L 1024  // large branches (C2: P = 8028, m = 2000; wide / generic)
 
 // Recompute the fused-path constants of branch b from theta: per column k of
 // W0 the power-of-two scale s_k, the four signed 7-bit digits of
 // (W0_jk / sigma_j) / s_k in the MFMA A-operand layout, and c0_k.
-__device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& bd, double* redd, float* redf) {
-  (void)redd;
-  (void)redf;
-  __shared__ float s_mx[4][UPD_THREADS / 64];
-  __shared__ double s_cs[4][UPD_THREADS / 64];
+template <int NT>
+__device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& bd) {
+  __shared__ float s_mx[4][NT / 64];
+  __shared__ double s_cs[4][NT / 64];
   const float* W0 = st.theta + bd.p_off + bd.woff[0];
   const float* b0 = st.theta + bd.p_off + bd.boff[0];
   const float* mu = st.mu + bd.mk_off;
@@ -67,7 +43,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
     const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
     double cs[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int j = threadIdx.x; j < m; j += UPD_THREADS) {
+    for (int j = threadIdx.x; j < m; j += NT) {
       const float sj = sg[j];
       const double mj = (double)mu[j];
 #pragma unroll
@@ -98,7 +74,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
     for (int q = 0; q < 4; ++q) {
       float M = s_mx[q][0];
       double C = s_cs[q][0];
-      for (int w = 1; w < UPD_THREADS / 64; ++w) {
+      for (int w = 1; w < NT / 64; ++w) {
         M = fmaxf(M, s_mx[q][w]);
         C += s_cs[q][w];
       }
@@ -115,7 +91,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
         st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
       }
     }
-    for (int j = threadIdx.x; j < m; j += UPD_THREADS) {
+    for (int j = threadIdx.x; j < m; j += NT) {
       const float sj = sg[j];
       const int c = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
 #pragma unroll
@@ -142,7 +118,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
 }
 
 // NV doubles summed over the workgroup in one pass (one barrier pair)
-template <int NV>
+template <int NT, int NV>
 __device__ void block_sum_n(double (&v)[NV], double* red) {
 #pragma unroll
   for (int q = 0; q < NV; ++q)
@@ -152,12 +128,12 @@ __device__ void block_sum_n(double (&v)[NV], double* red) {
   __syncthreads();
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int q = 0; q < NV; ++q) red[q * (UPD_THREADS / 64) + w] = v[q];
+    for (int q = 0; q < NV; ++q) red[q * (NT / 64) + w] = v[q];
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < NV; ++q) {
     double t = 0.0;
-    for (int k = 0; k < UPD_THREADS / 64; ++k) t += red[q * (UPD_THREADS / 64) + k];
+    for (int k = 0; k < NT / 64; ++k) t += red[q * (NT / 64) + k];
     v[q] = t;
   }
 }
@@ -171,16 +147,17 @@ __device__ void block_sum_n(double (&v)[NV], double* red) {
 // seven dependent global round trips (the launch follows a genotype stream that
 // has evicted all of it from L2).  Same arithmetic as the general path below.
 #define UPD_CAP 8
+template <int NT, int MPT>
 __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int mode, bool prof, int step,
                              double* redd, float* s_th) {
   const int P = bd.P, m = bd.m, w0 = bd.widths[0];
   const int64_t base = bd.p_off;
   const int t = threadIdx.x;
   // marker statistics for the refresh, prefetched
-  float mus[2], sgs[2];
+  float mus[MPT], sgs[MPT];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int j = t + c * UPD_THREADS;
+  for (int c = 0; c < MPT; ++c) {
+    const int j = t + c * NT;
     mus[c] = j < m ? st.mu[bd.mk_off + j] : 0.f;
     sgs[c] = j < m ? st.sigma[bd.mk_off + j] : 0.f;
   }
@@ -192,7 +169,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   double sums[3] = {0.0, 0.0, 0.0};
 #pragma unroll
   for (int c = 0; c < UPD_CAP; ++c) {
-    const int i = t + c * UPD_THREADS;
+    const int i = t + c * NT;
     th[c] = gr[c] = pm[c] = ep[c] = t0[c] = 0.f;
     if (i >= P) continue;
     float d = 0.f;
@@ -218,14 +195,14 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   }
   if (mode == MODE_GRAD) {
     double v1[1] = {sums[0]};
-    block_sum_n<1>(v1, redd);
+    block_sum_n<NT, 1>(v1, redd);
     if (t == 0) {
       st.ld_out[b] = v1[0] - (double)le * rss / 2.0;
       st.rss_out[b] = rss;
     }
     return;
   }
-  block_sum_n<3>(sums, redd);
+  block_sum_n<NT, 3>(sums, redd);
   const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
   const double h = ld - 0.5 * sums[1];                   // -H (878-883)
   const int stride = st.lint + 1;
@@ -264,7 +241,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   }
 #pragma unroll
   for (int c = 0; c < UPD_CAP; ++c) {
-    const int i = t + c * UPD_THREADS;
+    const int i = t + c * NT;
     if (i >= P) continue;
     float tn = th[c];
     if (act == 0) {  // (next) first half step + position step (params.rs:728-738)
@@ -294,8 +271,8 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   float mx[4] = {0.f, 0.f, 0.f, 0.f};
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int j = t + c * UPD_THREADS;
+  for (int c = 0; c < MPT; ++c) {
+    const int j = t + c * NT;
     if (j >= m) continue;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -305,8 +282,8 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
         cs[q] += (double)mus[c] * (double)wp;
       }
   }
-  __shared__ float s_mx[4][UPD_THREADS / 64];
-  __shared__ double s_cs[4][UPD_THREADS / 64];
+  __shared__ float s_mx[4][NT / 64];
+  __shared__ double s_cs[4][NT / 64];
   const int wv = t >> 6;
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -327,7 +304,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   for (int q = 0; q < 4; ++q) {
     float M = s_mx[q][0];
     double C = s_cs[q][0];
-    for (int w = 1; w < UPD_THREADS / 64; ++w) {
+    for (int w = 1; w < NT / 64; ++w) {
       M = fmaxf(M, s_mx[q][w]);
       C += s_cs[q][w];
     }
@@ -345,8 +322,8 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   }
   uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int j = t + c * UPD_THREADS;
+  for (int c = 0; c < MPT; ++c) {
+    const int j = t + c * NT;
     if (j >= m) continue;
     const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
 #pragma unroll
@@ -374,10 +351,9 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
 // reduction per scalar and re-read each array per phase: ~40 us per launch,
 // 18 % of a step at 125 branches per GPU.)  MODE_PROFILE repeats STEP's work
 // without changing the chain (bann_profile_session).
-__global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32_t* __restrict__ blist, int mode,
-                                                        int step) {
-  __shared__ double redd[4 * (UPD_THREADS / 64)];
-  __shared__ float redf[UPD_THREADS / 64];
+template <int NT, int MPT>
+__global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __restrict__ blist, int mode, int step) {
+  __shared__ double redd[4 * (NT / 64)];
   const int b = blist[blockIdx.x];
   const BranchDev bd = st.br[b];
   const int P = bd.P;
@@ -385,9 +361,9 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
   const bool prof = mode == MODE_PROFILE;
   if (prof) mode = MODE_STEP;
   if (!prof && (mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
-  if (bd.fused == 1 && P <= UPD_CAP * UPD_THREADS && bd.m <= 2 * UPD_THREADS && bd.widths[0] <= 4) {
-    __shared__ float s_th[UPD_CAP * UPD_THREADS];
-    update_small(st, b, bd, mode, prof, step, redd, s_th);
+  if ((bd.fused == 1 || bd.fused == 3) && P <= UPD_CAP * NT && bd.m <= MPT * NT && bd.widths[0] <= 4) {
+    __shared__ float s_th[UPD_CAP * NT];
+    update_small<NT, MPT>(st, b, bd, mode, prof, step, redd, s_th);
     return;
   }
 
@@ -400,7 +376,7 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
   // sum p^2 (momentum.rs:149-158; INIT: the drawn momentum, else the
   // half-stepped one), sums[2] = sum (theta - theta0) . p (551-592)
   double sums[3] = {0.0, 0.0, 0.0};
-  for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
+  for (int i = threadIdx.x; i < P; i += NT) {
     float d = 0.f;
     for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
     const float th = st.theta[base + i];
@@ -423,14 +399,14 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
   }
   if (mode == MODE_GRAD) {
     double v1[1] = {sums[0]};
-    block_sum_n<1>(v1, redd);
+    block_sum_n<NT, 1>(v1, redd);
     if (threadIdx.x == 0) {
       st.ld_out[b] = v1[0] - (double)le * rss / 2.0;
       st.rss_out[b] = rss;
     }
     return;
   }
-  block_sum_n<3>(sums, redd);
+  block_sum_n<NT, 3>(sums, redd);
   const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
   const double h = ld - 0.5 * sums[1];                   // -H = log density - K (878-883)
   const int stride = st.lint + 1;
@@ -443,7 +419,7 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
       st.rss_out[b] = rss;
       st.ld_out[b] = ld;
     }
-    for (int i = threadIdx.x; i < P; i += UPD_THREADS) {  // first half step + full position step
+    for (int i = threadIdx.x; i < P; i += NT) {  // first half step + full position step
       const float e = st.eps[base + i];
       const float th = st.theta[base + i];
       st.theta0[base + i] = th;
@@ -456,13 +432,13 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
     const bool diverged = !prof && fabs(h - h0) > (double)st.max_dh;
     if (!prof && threadIdx.x == 0) st.htrace[(int64_t)b * stride + step] = h;
     if (diverged) {  // RejectedEarly: restore the initial params (1264-1279)
-      for (int i = threadIdx.x; i < P; i += UPD_THREADS) st.theta[base + i] = st.theta0[base + i];
+      for (int i = threadIdx.x; i < P; i += NT) st.theta[base + i] = st.theta0[base + i];
       if (threadIdx.x == 0) st.status[b] = ST_REJECTED_EARLY;
     } else {
       // U-turn diagnostic (1281-1284)
       if (!prof && threadIdx.x == 0 && sums[2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;
       if (mode == MODE_STEP) {  // next step's first half step + position step (params.rs:728-738)
-        for (int i = threadIdx.x; i < P; i += UPD_THREADS) {
+        for (int i = threadIdx.x; i < P; i += NT) {
           const float e = st.eps[base + i];
           const float g = st.grad[base + i];
           const float p = (prof ? st.mom[base + i] + st.eps[base + i] * 0.5f * g : st.mom[base + i]) + 0.5f * e * g;
@@ -478,7 +454,7 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
         const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
         const bool accept = (double)st.uacc[b] < acc_p;
         if (!accept)
-          for (int i = threadIdx.x; i < P; i += UPD_THREADS) st.theta[base + i] = st.theta0[base + i];
+          for (int i = threadIdx.x; i < P; i += NT) st.theta[base + i] = st.theta0[base + i];
         if (threadIdx.x == 0) {
           st.status[b] = accept ? ST_ACCEPTED : ST_REJECTED;
           st.ld_out[b] = ld;
@@ -490,22 +466,26 @@ __global__ void __launch_bounds__(UPD_THREADS) k_update(DevState st, const int32
   if (bd.fused) {
     __syncthreads();
     __threadfence_block();
-    refresh_fused_const(st, b, bd, redd, redf);
+    refresh_fused_const<NT>(st, b, bd);
   }
 }
 
+// small: branches with P <= 2048 and m <= 512 (256 threads); large: the rest (1024 threads)
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
-                   hipStream_t s) {
+                   hipStream_t s, int large) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(k_update, dim3(nb), dim3(UPD_THREADS), 0, s, st, branches, mode, step);
+  if (large)
+    hipLaunchKernelGGL((k_update<UPD_THREADS_L, 4>), dim3(nb), dim3(UPD_THREADS_L), 0, s, st, branches, mode, step);
+  else
+    hipLaunchKernelGGL((k_update<UPD_THREADS, 2>), dim3(nb), dim3(UPD_THREADS), 0, s, st, branches, mode, step);
 }
 
+bool update_is_large(const BranchDev& d) { return d.P > UPD_CAP * UPD_THREADS || d.m > 2 * UPD_THREADS; }
+
 __global__ void __launch_bounds__(UPD_THREADS) k_fused_const(DevState st, const int32_t* __restrict__ blist) {
-  __shared__ double redd[UPD_THREADS / 64];
-  __shared__ float redf[UPD_THREADS / 64];
   const int b = blist[blockIdx.x];
   const BranchDev bd = st.br[b];
-  if (bd.fused) refresh_fused_const(st, b, bd, redd, redf);
+  if (bd.fused) refresh_fused_const<UPD_THREADS>(st, b, bd);
 }
 
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s) {
@@ -526,6 +506,20 @@ __global__ void k_sample_momentum(DevState st, const int32_t* __restrict__ blist
   sincosf(6.283185307179586f * u2, &sn, &cs);
   st.mom[bd.p_off + 2 * i2] = rad * cs;
   if (2 * i2 + 1 < bd.P) st.mom[bd.p_off + 2 * i2 + 1] = rad * sn;
+}
+
+// Metropolis uniforms, one per branch (accept_or_reject_hmc_state's ThreadRng
+// draw, branch_sampler.rs:546-548): Philox, independent of the momentum stream
+__global__ void k_uniforms(DevState st, const int32_t* __restrict__ blist, int nb, uint64_t seed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  const int b = blist[i];
+  st.uacc[b] = u01(philox_bits(seed, 0xACCE97ull, (uint64_t)b).x);
+}
+
+void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_uniforms, dim3((nb + 255) / 256), dim3(256), 0, s, st, branches, nb, seed);
 }
 
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
