@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)                       # rs-bann_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.environ.get("BANN_LIB", os.path.join(PKG_ROOT, "librsbann_amd.so"))
+LIB_PATH = os.environ.get("BANN_LIB") or os.path.join(PKG_ROOT, "librsbann_amd.so")
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "bann.h")
 HEADER_PATHS = [HEADER_PATH, os.path.join(REPO_ROOT, "include", "bann_net.h")]
 

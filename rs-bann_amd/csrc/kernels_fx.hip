@@ -682,6 +682,15 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 // registers two chunks ahead with counted loads instead of an LDS image.
 // ===========================================================================
 #define FXL_MAXW 8
+#ifndef FXL_PD
+#define FXL_PD 8  // backward genotype-window prefetch depth
+#endif
+#ifndef FXL_DPRE
+#define FXL_DPRE 31  // backward window after which the next tile's first digit loads issue (earlier: spills)
+#endif
+#ifndef FXL_ABL
+#define FXL_ABL 0  // profiling-only ablations (1: no W0 digit loads, 2: no per-tile barrier); 0 in shipped builds
+#endif
 
 // one global_load_dwordx4 outside the compiler's wait model (counted by hand)
 __device__ __forceinline__ v4i ld_counted(const char* p) {
@@ -805,6 +814,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     issue_y(tt, 0);
   }
   auto ldig = [&](int off) -> v4i {
+#if FXL_ABL & 1
+    return v4i{off, 1, 2, 3};  // profiling build: no digit loads
+#endif
     if constexpr (CNT) return ld_counted(dsrc + off);
     return *reinterpret_cast<const v4i*>(dsrc + off);
   };
@@ -829,7 +841,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
         v4u Xn = Xc;
         if (c + 1 < 8 && (FULL || c + 1 < cw))
           Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
-        if constexpr (CNT) {
+        if constexpr (CNT && !(FXL_ABL & 1)) {
           // loads younger than digit load c (issue order below: D(c+2) then
           // piece c per chunk, the pieces issued on every tile so the count is a
           // compile-time constant -- a runtime count would need a branch, and the
@@ -865,7 +877,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     // ---- Z0 exchange: every wave sums the NW partials in wave order ----
     v4f* xw = s_xch + (xb * NW) * 64;
     lds_st_v4f(xw + wave * 64 + lane, v4f{z0, z1, z2, z3});
+#if !(FXL_ABL & 2)
     LDS_BARRIER();
+#endif
     {
       v4f zs = xw[lane];
       for (int w = 1; w < NW; ++w) zs += xw[w * 64 + lane];
@@ -998,7 +1012,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     // ---- backward: dW0 digit sums of this wave's block += G^T delta0 ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
-      constexpr int PD = 8;
+      constexpr int PD = FXL_PD;
       uint32_t wq[PD];
 #pragma unroll
       for (int u = 0; u < PD; ++u)
@@ -1013,12 +1027,12 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
                            (int)((wv >> 6) & 0x03030303u)};
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
+        // the next tile's first two digit operands, half a backward ahead of their use
+        if (u == FXL_DPRE && more) {
+          Dn0 = ldig(0);
+          if (FULL || cw > 1) Dn1 = ldig(1024);
+        }
       }
-    }
-    // the next tile's first two digit operands
-    if (more) {
-      Dn0 = ldig(0);
-      if (FULL || cw > 1) Dn1 = ldig(1024);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -1,0 +1,38 @@
+"""Build-time guards for the hand-counted memory waits of the fxl kernel.
+
+k_fused_grad_fxl<NL <= 3, ACT, FULL = 1> loads its W0-digit operands with inline
+asm and waits on them with hand-counted ``s_waitcnt vmcnt`` (kernels_fx.hip).  A
+register spill of such an operand while its load is in flight would store
+garbage, so those instantiations must compile without VGPR spills.  (CPU test:
+hipcc cross-compiles gfx950 here.)"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "rs-bann_amd", "csrc", "kernels_fx.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_counted_fxl_instantiations_do_not_spill(tmp_path):
+    out = subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics",
+                          "-c", SRC, "-o", str(tmp_path / "k.o"), "-Rpass-analysis=kernel-resource-usage"],
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    spills, name = {}, None
+    for line in out.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.search(r"VGPRs Spill: (\d+)", line)
+        if m and name:
+            spills[name] = int(m.group(1))
+    counted = [k for k in spills if re.match(r"_Z16k_fused_grad_fxlILi[23]ELi\dELi1E", k)]
+    assert len(counted) == 10, counted
+    assert all(spills[k] == 0 for k in counted), {k: spills[k] for k in counted}
+    fx = [k for k in spills if k.startswith("_Z15k_fused_grad_fx")]
+    assert fx and all(spills[k] == 0 for k in fx), {k: spills[k] for k in fx}

@@ -30,6 +30,7 @@ for b in range(a.branches):
 ctx.leapfrog_begin(list(range(a.branches)), 2, 10.0, "izmailov", 0.1, seed=1)
 ctx.profile_session(2)
 g, u = ctx.profile_session(a.iters)
-xb = a.n * a.m * a.branches
-print(json.dumps(dict(tag=a.tag, lib=os.environ.get("BANN_LIB", "default"), grad_ms=g, update_ms=u,
-                      x_GBps=xb / g / 1e6, alg_GBps=(xb + 4 * a.n * a.branches) / g / 1e6)))
+xb = ((a.n + 3) // 4) * a.m * a.branches   # 2-bit genotypes (the .bed payload size)
+print(json.dumps(dict(tag=a.tag, lib=os.environ.get("BANN_LIB", "default"), branches=a.branches, n=a.n, m=a.m,
+                      path=ctx.kernel_path(0), grad_ms=round(g, 4), update_ms=round(u, 4),
+                      alg_GBps=round((xb + 4 * a.n * a.branches) / g / 1e6, 1))), flush=True)
