@@ -92,7 +92,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)   # L = 100: the reference default integration length (mcmc_cfg.rs:38)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--step-factor", type=float, default=1.0)   # cli.rs:99-100 default
+    ap.add_argument("--step-factor", type=float, default=None,
+                    help="Izmailov factor c; default 1.0 (cli.rs:99-100), 0.15 for c5 (acceptance ~0.7 at L = 100)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-branches", type=int, default=96)   # capped at the config's branch count
     ap.add_argument("--cpu-sample-steps", type=int, default=16)
@@ -121,6 +122,10 @@ def main():
     from bann.distributed import allreduce_sum_, shard_ranges
 
     n, M_total, B_total, widths = CONFIGS[args.config]
+    if args.step_factor is None:
+        # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
+        # curvature, c = 1 rejects every trajectory; c = 0.15 accepts ~0.7
+        args.step_factor = 0.15 if args.config == "c5" else 1.0
     m_b = M_total // B_total
     b0, b1 = shard_ranges([m_b] * B_total, max(world, args.emulate_shard))[rank]   # contiguous, balanced by markers
     nb = b1 - b0
@@ -248,11 +253,12 @@ def main():
     i8_ops = 2 * 2 * n * m_b * 4 * widths[0] * nb
     # HBM traffic per gradient launch, from the committed PMC pass of the same
     # workload (tools/profile_round.sh; a --pmc run cannot time itself)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, mfma_pmc = None, None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         pm = json.load(open(f))
         if world == 1 and not args.emulate_shard and pm.get("config", "").split(":")[0] == workload.split(":")[0] and pm.get("kernel", "").startswith(f"void {kernel_name}<"):
             traffic, traffic_src = pm["traffic_bytes_per_launch"], os.path.relpath(f, ROOT)
+            mfma_pmc = pm.get("mfma")
             break
 
     cpu = None
@@ -291,6 +297,7 @@ def main():
                           (BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF),
                           "basis": "hidden-layer GEMM flops 6 n W S per branch per launch",
                           "i8_mfma_tops": i8_ops / (grad_ms * 1e-3) / 1e12,
+                          "mfma_busy_pmc": (mfma_pmc or {}).get("mfma_busy_per_simd_cycle"),
                           "hbm_GBps": achieved} if wide else
                          {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": achieved / HBM_PEAK_GBS}) | {"traffic": traffic,
@@ -300,6 +307,7 @@ def main():
                          "alg_bytes_basis": "2-bit genotypes (n*m_b/4) + 4n target bytes per branch", "update_kernel_ms": upd_ms},
             "cpu_baseline": cpu,
             "accept_rate": acc_all / nb_all,
+            "step_factor": args.step_factor,
             "setup_s": setup_s,
         }
         if args.emulate_shard:

@@ -58,6 +58,27 @@ pmc = {"kernel": full[0]["Kernel_Name"], "config": bench["config"]["workload"],
        "note": "FETCH_SIZE x 2 (gfx950 wide-read correction, MI355X_MICROARCH.md HBM), WRITE_SIZE as reported; "
                "fetch: median over the full-branch-set launches of a separate --pmc pass; write: the steady-state "
                "leapfrog launch (min; the trajectory's first and last launch also write predictions)"}
+mf = find("mfma", "*counter_collection.csv")
+if mf:  # MFMA utilisation pass: per-counter medians over the full-branch-set gradient launches
+    per = {}
+    for r in csv.DictReader(open(mf)):
+        if "k_fused_grad" not in r["Kernel_Name"]:
+            continue
+        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        d = per.setdefault(key, {"grid": int(r.get("Grid_Size", 0) or 0)})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    gmax = max(d["grid"] for d in per.values())
+    sel = [d for d in per.values() if d["grid"] == gmax]
+    names = sorted({k for d in sel for k in d if k != "grid"})
+    med = {k: statistics.median(d.get(k, 0.0) for d in sel) for k in names}
+    cycles = med.get("GRBM_GUI_ACTIVE", 0.0) / 8.0   # rocprofv3 sums GRBM over the 8 XCDs
+    busy = med.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+    pmc["mfma"] = {"counters_median_per_launch": med,
+                   "kernel_cycles": cycles,
+                   "mfma_busy_per_simd_cycle": busy / (cycles * 1024) if cycles else None,
+                   "mfma_busy_per_cu_cycle": busy / (cycles * 256) if cycles else None,
+                   "note": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x SIMDs or CUs): the matrix pipes' busy "
+                           "fraction over the launch; MOPS counters are the MFMA operation counts per launch"}
 json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
 
 with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
@@ -76,6 +97,12 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
             f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
     f.write(f"achieved (algorithmic bytes / median launch): "
             f"{pmc['alg_bytes_per_launch'] / (statistics.median(dur) * 1e-3) / 1e9:.0f} GB/s\n\n")
+    if "mfma" in pmc:
+        m = pmc["mfma"]
+        f.write("MFMA pass (median per gradient launch): " +
+                ", ".join(f"{k} {v:.4g}" for k, v in m["counters_median_per_launch"].items()) +
+                f"; matrix-pipe busy fraction {m['mfma_busy_per_simd_cycle']:.3f} per SIMD-cycle "
+                f"({m['mfma_busy_per_cu_cycle']:.3f} per CU-cycle)\n\n")
     f.write("Full per-kernel stats of the command (all launches, setup included): "
             f"`{tag}_kernel_stats.csv`.\n")
 print(open(os.path.join(prof, f"{tag}_summary.md")).read())
