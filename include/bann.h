@@ -171,6 +171,32 @@ int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L,
                   const float* u, int32_t* status_out, double* h_trace_out, int32_t* uturn_out,
                   double* log_density_out);
 
+/* ---------------- joint HMC: replaces hmc_step_joint (branch_sampler.rs:1070-1178) ----------------
+ * One trajectory per listed branch over its parameters AND its precisions
+ * (ridge / lasso priors; std_normal has no joint density and is refused),
+ * packed like bann_hmc_step.  The precisions start from the branch's precision
+ * vector and the sampled ones become its precisions (bann_branch_get_precisions).
+ *   hyper: 6 floats, NetworkPrecisionHyperparameters (params.rs:134-142):
+ *       dense (shape, scale), summary (shape, scale), output (shape, scale)
+ *   step_mode == BANN_STEP_INJECTED: eps = per branch [num_params | num_precisions]
+ *       step sizes; any other mode: random step sizes U(0,1) (P+Q)^-1/4 factor
+ *       drawn from seed (the reference joint sampler falls back to random for
+ *       every mode, 1092-1101)
+ *   momentum: per branch [num_params | num_precisions], or NULL (device N(0,1))
+ *   u: acceptance uniform per branch, or NULL (drawn from seed)
+ * The early-rejection test uses the joint -H; the final Metropolis test uses the
+ * NON-joint log_density against the joint initial -H, as accept_or_reject_hmc_state
+ * (928-962) does.  log_density_out: the non-joint log density of the final
+ * state.  L >= 1. */
+int bann_hmc_step_joint(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_hamiltonian_error,
+                        int32_t step_mode, float step_factor, const float* eps, const float* momentum, uint64_t seed,
+                        const float* u, const float* hyper, int32_t* status_out, double* h_trace_out,
+                        double* log_density_out);
+/* OutputWeightSummaryStats of branch b (params.rs:404-465) for the joint density
+ * of the output layer: the reg sum of the OTHER branches' output weights and the
+ * network's output-weight count (default 0 and the branch's own count). */
+int bann_branch_set_output_stats(bann_ctx* ctx, int32_t b, float reg_sum_others, float num_params);
+
 /* ---------------- benchmark / production leapfrog stepping ----------------
  * Device-resident trajectory state for a fixed branch set: begin samples the
  * momenta on the device and evaluates the initial gradient and -H; each

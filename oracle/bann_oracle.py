@@ -563,6 +563,86 @@ def hmc_step(br: Branch, X, y, eps_w, eps_b, p_w, p_b, L_int: int, max_dH: float
 
 
 # --------------------------------------------------------------------------
+# joint HMC over parameters and precisions: branch_sampler.rs:1070-1178
+# --------------------------------------------------------------------------
+def load_precision_vec(br: Branch, vec) -> None:
+    """inverse of precision_vec (params.rs:272-289), in place."""
+    vec = np.asarray(vec, dtype=np.float64)
+    ix, wp = 0, []
+    for p in br.weight_precisions:
+        shp = np.asarray(p).shape
+        k = int(np.prod(shp)) if shp else 1
+        wp.append(vec[ix:ix + k].reshape(shp).copy())
+        ix += k
+    nb = len(br.bias_precisions)
+    br.weight_precisions = wp
+    br.bias_precisions = [float(v) for v in vec[ix:ix + nb]]
+    br.error_precision = float(vec[ix + nb])
+
+
+def ldg_joint_vec(br: Branch, X, y, hp: Hyper):
+    """log_density_gradient_joint (branch_sampler.rs:406-422) as one vector:
+    [param_vec order | precision_vec order], and the rss."""
+    g = ldg_joint(br, X, y, hp)
+    gph = [np.asarray(x, dtype=np.float64).reshape(-1) for x in g["wrt_weight_precisions"]]
+    gph += [np.asarray(g["wrt_bias_precisions"], dtype=np.float64).reshape(-1),
+            np.asarray([g["wrt_error_precision"]], dtype=np.float64)]
+    return np.concatenate([param_vec(g["wrt_weights"], g["wrt_biases"])] + gph), g["rss"]
+
+
+def hmc_step_joint(br: Branch, X, y, hp: Hyper, eps, p, L_int: int, max_dH: float, u: float):
+    """hmc_step_joint (branch_sampler.rs:1070-1178): leapfrog over the parameters
+    AND the precisions (params.full_step + precisions.full_step, 1116-1117), -H
+    from log_density_joint (886-901), early rejection on the joint -H, then
+    accept_or_reject_hmc_state (928-962), whose final -H uses the NON-joint
+    log_density -- a reference quirk reproduced here.  eps, p: concatenated
+    [param_vec | precision_vec] step sizes and momenta (injected draws).
+    ``br`` is updated in place (restored on rejection)."""
+    n = y.size
+    P = br.num_params
+    init = br.copy()
+    eps = np.asarray(eps, dtype=np.float64)
+    p = np.array(p, dtype=np.float64)
+
+    def state():
+        return np.concatenate([param_vec(br.weights, br.biases), precision_vec(br)])
+
+    def set_state(v):
+        br.weights, br.biases = load_param_vec(v[:P], br.num_markers, br.layer_widths)
+        load_precision_vec(br, v[P:])
+
+    def neg_h():
+        with np.errstate(all="ignore"):
+            return log_density_joint(br, rss(br, X, y), hp, n) - 0.5 * float(p @ p)
+
+    H0 = neg_h()
+    g, _ = ldg_joint_vec(br, X, y, hp)
+    trace = [H0]
+    for step in range(L_int):
+        p += 0.5 * eps * g                                             # 1114
+        set_state(state() + eps * p)                                   # 1115-1116
+        with np.errstate(all="ignore"):
+            g, _ = ldg_joint_vec(br, X, y, hp)                         # 1118
+        p += 0.5 * eps * g                                             # 1119
+        H = neg_h()                                                    # 1123-1124
+        trace.append(H)
+        if abs(H - H0) > max_dH:                                       # 1138-1158 (NaN never exceeds)
+            br.weights, br.biases = init.weights, init.biases
+            load_precision_vec(br, precision_vec(init))
+            return dict(status=REJECTED_EARLY, trace=trace, step=step)
+    r = predict(br, X) - y
+    with np.errstate(all="ignore"):
+        ld = log_density(br, float(np.sum(r * r)))                     # non-joint (943)
+        log_acc = (ld - 0.5 * float(p @ p)) - H0
+        acc_p = 1.0 if log_acc >= 0 else math.exp(log_acc)
+    if u < acc_p:
+        return dict(status=ACCEPTED, trace=trace, log_density=ld, p=p)
+    br.weights, br.biases = init.weights, init.biases
+    load_precision_vec(br, precision_vec(init))
+    return dict(status=REJECTED, trace=trace, log_density=ld, p=p)
+
+
+# --------------------------------------------------------------------------
 # Gibbs precision posteriors (host side): gibbs_steps.rs, ridge_ard.rs:271-301
 # --------------------------------------------------------------------------
 def ridge_posterior_params(shape: float, scale: float, sum_sq: float, num: int):

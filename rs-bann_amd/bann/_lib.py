@@ -104,6 +104,9 @@ SIGNATURES = {
     "bann_neg_hamiltonian": (C.c_int, [_P, _i32, _pf32, _pf64]),
     "bann_hmc_step": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pi32, _pf64,
                                 _pi32, _pf64]),
+    "bann_hmc_step_joint": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pf32,
+                                      _pi32, _pf64, _pf64]),
+    "bann_branch_set_output_stats": (C.c_int, [_P, _i32, _f32, _f32]),
     "bann_leapfrog_begin": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _u64]),
     "bann_leapfrog_steps": (C.c_int, [_P, _i32]),
     "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),

@@ -68,7 +68,15 @@ class BannContext:
         self.n, self.num_markers = n, M
 
     def upload_bed(self, payload: bytes, n: int, num_markers: int):
-        buf = np.frombuffer(bytes(payload), dtype=np.uint8).copy()
+        """variant-major .bed payload, ceil(n/4) bytes per marker; a full .bed file's
+        3-byte signature (0x6c 0x1b 0x01, bed.rs:100-116) is stripped."""
+        data = bytes(payload)
+        want = ((n + 3) // 4) * num_markers
+        if len(data) == want + 3 and data[:3] == b"\x6c\x1b\x01":
+            data = data[3:]
+        if len(data) != want:
+            raise ValueError(f".bed payload has {len(data)} bytes, n={n} x {num_markers} markers need {want}")
+        buf = np.frombuffer(data, dtype=np.uint8).copy()
         self._check(self._lib.bann_genotypes_upload_bed(self._h, _ptr(buf, C.c_uint8), n, num_markers))
         self.n, self.num_markers = n, num_markers
 
@@ -202,9 +210,20 @@ class BannContext:
 
     def neg_hamiltonian(self, b: int, momentum) -> float:
         p = _f32(momentum)
+        if p.size != self.num_params(b):
+            raise ValueError(f"momentum has {p.size} entries, branch {b} has {self.num_params(b)} parameters")
         out = C.c_double()
         self._check(self._lib.bann_neg_hamiltonian(self._h, b, _ptr(p, C.c_float), C.byref(out)))
         return out.value
+
+    def _check_sizes(self, br, eps, momentum, u, extra=None):
+        """the C side reads sum(P_b) (+ extra(b)) floats of eps / momentum and one uniform per branch"""
+        tot = sum(self.num_params(int(b)) + (extra(int(b)) if extra else 0) for b in br)
+        for name, a in (("eps", eps), ("momentum", momentum)):
+            if a is not None and a.size != tot:
+                raise ValueError(f"{name} has {a.size} entries, the branches need {tot}")
+        if u is not None and u.size != br.size:
+            raise ValueError(f"u has {u.size} entries, expected one per branch ({br.size})")
 
     def hmc_step(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,
                  step_mode: str = "izmailov", step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0,
@@ -215,6 +234,7 @@ class BannContext:
         eps_a = _f32(eps) if eps is not None else None
         mom_a = _f32(momentum) if momentum is not None else None
         u_a = _f32(u) if u is not None else None
+        self._check_sizes(br, eps_a, mom_a, u_a)
         status = np.zeros(nb, np.int32)
         trace = np.zeros((nb, L + 1), np.float64)
         uturn = np.zeros(nb, np.int32)
@@ -228,6 +248,37 @@ class BannContext:
             _ptr(u_a, C.c_float) if u_a is not None else nullf,
             _ptr(status, C.c_int32), _ptr(trace, C.c_double), _ptr(uturn, C.c_int32), _ptr(ld, C.c_double)))
         return dict(status=status, trace=trace, uturn=uturn, log_density=ld)
+
+    def set_output_stats(self, b: int, reg_sum_others: float, num_params: float):
+        """OutputWeightSummaryStats of branch b for the joint density (params.rs:404-465)."""
+        self._check(self._lib.bann_branch_set_output_stats(self._h, b, float(reg_sum_others), float(num_params)))
+
+    def hmc_step_joint(self, branches: Sequence[int], L: int, hyper, max_hamiltonian_error: float = 10.0,
+                       step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0, u=None):
+        """hmc_step_joint (branch_sampler.rs:1070-1178): parameters and precisions.
+        hyper: (dense shape, scale, summary shape, scale, output shape, scale);
+        eps / momentum: per branch [num_params | num_precisions] (or None)."""
+        br = np.ascontiguousarray(branches, dtype=np.int32)
+        nb = br.size
+        eps_a = _f32(eps) if eps is not None else None
+        mom_a = _f32(momentum) if momentum is not None else None
+        u_a = _f32(u) if u is not None else None
+        hp = _f32(hyper)
+        if hp.size != 6:
+            raise ValueError("hyper needs 6 values")
+        self._check_sizes(br, eps_a, mom_a, u_a, extra=self.num_precisions)
+        status = np.zeros(nb, np.int32)
+        trace = np.zeros((nb, L + 1), np.float64)
+        ld = np.zeros(nb, np.float64)
+        mode = STEP_MODES["injected"] if eps is not None else STEP_MODES["random"]
+        nullf = C.POINTER(C.c_float)()
+        self._check(self._lib.bann_hmc_step_joint(
+            self._h, _ptr(br, C.c_int32), nb, L, max_hamiltonian_error, mode, step_factor,
+            _ptr(eps_a, C.c_float) if eps_a is not None else nullf,
+            _ptr(mom_a, C.c_float) if mom_a is not None else nullf, seed,
+            _ptr(u_a, C.c_float) if u_a is not None else nullf, _ptr(hp, C.c_float),
+            _ptr(status, C.c_int32), _ptr(trace, C.c_double), _ptr(ld, C.c_double)))
+        return dict(status=status, trace=trace, log_density=ld)
 
     # ------------------------------------------------------ leapfrog session
     def leapfrog_begin(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,

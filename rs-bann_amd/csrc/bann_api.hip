@@ -28,6 +28,8 @@ struct BranchHost {
   int32_t m = 0, L = 0, act = 0, prior = 0;
   int32_t P = 0, nprec = 0;
   std::vector<float> prec;  // precision_vec order
+  float ows_reg_sum = 0.f;  // output-weight summary stat of the OTHER branches (joint HMC)
+  float ows_num = -1.f;     // output-weight count of the network (< 0: this branch's own)
   BranchDev dev{};
 };
 
@@ -78,6 +80,10 @@ struct bann_ctx {
   double* d_rss_part = nullptr;
   float* d_pred0 = nullptr;
   double* d_stepbase = nullptr;  // per-parameter Izmailov step base (sign: factor applies)
+  float *d_phi = nullptr, *d_phi0 = nullptr, *d_mphi = nullptr, *d_ephi = nullptr, *d_gphi = nullptr;  // joint HMC
+  int32_t* d_pidx = nullptr;
+  float* d_ows = nullptr;
+  int64_t total_q = 0;
   float* d_delta = nullptr;       // n floats: residual change of the last trajectory (host-copy variant)
   float* d_delta_part = nullptr;  // per-branch-slice partial rows of the residual change
   int32_t* h_status = nullptr;    // pinned host mirrors (trajectory status, residual change)
@@ -169,6 +175,13 @@ static void refresh_state(bann_ctx* ctx) {
   s.nfrag = ctx->nfrag;
   s.max_splits = ctx->max_splits;
   s.lint = ctx->htrace_cap - 1;
+  s.phi = ctx->d_phi;
+  s.phi0 = ctx->d_phi0;
+  s.mphi = ctx->d_mphi;
+  s.ephi = ctx->d_ephi;
+  s.gphi = ctx->d_gphi;
+  s.pidx = ctx->d_pidx;
+  s.ows = ctx->d_ows;
 }
 
 static bool check_branch(const bann_ctx* ctx, int32_t b) {
@@ -416,7 +429,8 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
-                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase};
+                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
+                  ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows};
   for (void* p : bufs) dfree(p);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
@@ -700,6 +714,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4), 8 / nw));
     fxl_splits[nw] = best_splits(nfxl[nw], per_cu * cus, 1);
   }
+  int64_t q_off = 0;
   int64_t x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
@@ -711,6 +726,18 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     if (d.fused) dig_off += (int64_t)d.nchunks * 1024 * (d.fused == 2 ? 8 : 1);
     d.p_off = p_off;
     p_off += h.P;
+    {  // precision coordinates in precision_vec order (params.rs:272-289)
+      const bool ard = (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD);
+      int qo = 0;
+      for (int l = 0; l < h.L; ++l) {
+        d.qoff[l] = qo;
+        qo += (ard && l < h.L - 1) ? d.win[l] : 1;
+      }
+      d.qbias = qo;
+      d.nq = qo + (h.L - 1) + 1;
+      d.q_off = q_off;
+      q_off += d.nq;
+    }
     d.mk_off = mk_off;
     mk_off += h.m;
     d.y_off = (int64_t)b * n;
@@ -746,6 +773,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   ctx->max_splits = max_splits;
   ctx->packed_bytes = x2_off;
   ctx->total_p = p_off;
+  ctx->total_q = q_off;
   const int64_t nb = (int64_t)ctx->br.size();
   CK(dalloc(&ctx->d_xu2, x2_off));
   CK(dalloc(&ctx->d_dig, dig_off));
@@ -761,6 +789,23 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     CK(hipMemsetAsync(*pb, 0, p_off * sizeof(float), ctx->stream));
   }
   CK(dalloc(&ctx->d_stepbase, p_off));
+  for (float** qb : {&ctx->d_phi, &ctx->d_phi0, &ctx->d_mphi, &ctx->d_ephi, &ctx->d_gphi}) CK(dalloc(qb, q_off));
+  CK(dalloc(&ctx->d_ows, 2 * (int64_t)ctx->br.size()));
+  {  // parameter -> precision index (within the branch), for the joint update
+    std::vector<int32_t> pidx(p_off);
+    for (auto& h : ctx->br) {
+      const BranchDev& d = h.dev;
+      const bool ard = (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD);
+      for (int l = 0; l < h.L; ++l)
+        for (int k = 0; k < d.widths[l]; ++k)
+          for (int j = 0; j < d.win[l]; ++j)
+            pidx[d.p_off + d.woff[l] + (int64_t)k * d.win[l] + j] = d.qoff[l] + ((ard && l < h.L - 1) ? j : 0);
+      for (int l = 0; l < h.L - 1; ++l)
+        for (int k = 0; k < d.widths[l]; ++k) pidx[d.p_off + d.boff[l] + k] = d.qbias + l;
+    }
+    CK(dalloc(&ctx->d_pidx, p_off));
+    CK(hipMemcpy(ctx->d_pidx, pidx.data(), p_off * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   CK(dalloc(&ctx->d_part, part_off));
   CK(hipMemsetAsync(ctx->d_part, 0, part_off * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_rss_part, nb * max_splits));
@@ -839,6 +884,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
 
 extern "C" int bann_branch_set_params(bann_ctx* ctx, int32_t b, const float* param_vec) {
   if (!check_branch(ctx, b) || !param_vec) return fail(ctx, BANN_E_ARG, "bad branch or null params");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
   const BranchHost& h = ctx->br[b];
   CK(hipMemcpyAsync(ctx->d_theta + h.dev.p_off, param_vec, h.P * sizeof(float), hipMemcpyHostToDevice,
                     ctx->stream));
@@ -858,10 +904,10 @@ extern "C" int bann_branch_get_params(bann_ctx* ctx, int32_t b, float* out) {
   return BANN_OK;
 }
 
-extern "C" int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float* prec) {
-  if (!check_branch(ctx, b) || !prec) return fail(ctx, BANN_E_ARG, "bad branch or null precisions");
-  BranchHost& h = ctx->br[b];
-  h.prec.assign(prec, prec + h.nprec);
+// device copies derived from the host precision vector h.prec: per-parameter
+// prior multipliers, error precision, Izmailov step bases
+static int upload_precisions(bann_ctx* ctx, int32_t b) {
+  const BranchHost& h = ctx->br[b];
   std::vector<float> lam, lamld;
   float ep = 1.f;
   expand_precisions(h, lam, lamld, ep);
@@ -874,6 +920,20 @@ extern "C" int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float*
   CK(hipMemcpyAsync(ctx->d_stepbase + h.dev.p_off, sbase.data(), h.P * sizeof(double), hipMemcpyHostToDevice,
                     ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_set_precisions(bann_ctx* ctx, int32_t b, const float* prec) {
+  if (!check_branch(ctx, b) || !prec) return fail(ctx, BANN_E_ARG, "bad branch or null precisions");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  ctx->br[b].prec.assign(prec, prec + ctx->br[b].nprec);
+  return upload_precisions(ctx, b);
+}
+
+extern "C" int bann_branch_set_output_stats(bann_ctx* ctx, int32_t b, float reg_sum_others, float num_params) {
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  ctx->br[b].ows_reg_sum = reg_sum_others;
+  ctx->br[b].ows_num = num_params;
   return BANN_OK;
 }
 
@@ -893,6 +953,7 @@ extern "C" int bann_branch_get_precisions(bann_ctx* ctx, int32_t b, float* out) 
 
 extern "C" int bann_branch_set_target(bann_ctx* ctx, int32_t b, const float* y) {
   if (!check_branch(ctx, b) || !y) return fail(ctx, BANN_E_ARG, "bad branch or null target");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
   CK(hipMemcpyAsync(ctx->d_y + (int64_t)b * ctx->n, y, ctx->n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   return BANN_OK;
@@ -900,6 +961,7 @@ extern "C" int bann_branch_set_target(bann_ctx* ctx, int32_t b, const float* y) 
 
 extern "C" int bann_set_target_all(bann_ctx* ctx, const float* y) {
   if (!ctx || !ctx->finalized || !y) return fail(ctx, BANN_E_ARG, "not finalized or null target");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
   for (size_t b = 0; b < ctx->br.size(); ++b)
     CK(hipMemcpyAsync(ctx->d_y + (int64_t)b * ctx->n, y, ctx->n * sizeof(float), hipMemcpyHostToDevice,
                       ctx->stream));
@@ -1113,9 +1175,101 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   return BANN_OK;
 }
 
+// hmc_step_joint (branch_sampler.rs:1070-1178): parameters AND precisions
+extern "C" int bann_hmc_step_joint(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
+                                   int32_t step_mode, float factor, const float* eps, const float* momentum,
+                                   uint64_t seed, const float* u, const float* hyper, int32_t* status_out,
+                                   double* h_trace_out, double* log_density_out) {
+  if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (!branches || nb <= 0 || L < 1 || !hyper) return fail(ctx, BANN_E_ARG, "bad branch list, L or hyperparameters");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  if (step_mode == BANN_STEP_INJECTED && !eps) return fail(ctx, BANN_E_ARG, "injected step sizes need eps");
+  Plan p;
+  int rc = build_plan(ctx, branches, nb, p, false);
+  if (rc) return rc;
+  int32_t max_q = 0;
+  for (int i = 0; i < nb; ++i) {
+    const BranchHost& h = ctx->br[branches[i]];
+    if (h.prior == BANN_STD_NORMAL)
+      return fail(ctx, BANN_E_ARG, "std_normal has no joint density (std_normal_branch.rs:119-131)");
+    if (h.dev.nq > BANN_JOINT_MAXQ) return fail(ctx, BANN_E_SHAPE, "too many precisions for the joint update");
+    max_q = std::max(max_q, h.dev.nq);
+  }
+  rc = ensure_htrace(ctx, L);
+  if (rc) return rc;
+  for (int k = 0; k < 6; ++k) ctx->st.hyper[k] = hyper[k];
+  ctx->st.max_dh = max_dh;
+  ctx->st.lint = ctx->htrace_cap - 1;
+  // host staging: precision coordinates, output-weight stats, step sizes, momenta, uniforms
+  std::vector<float> ows(2 * ctx->br.size(), 0.f), ep, mo, uu(ctx->br.size(), 0.f);
+  std::mt19937_64 rng(seed ^ 0x5DEECE66Dull);
+  std::uniform_real_distribution<float> U(0.f, 1.f);
+  int64_t off = 0;
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
+    const BranchHost& h = ctx->br[b];
+    const int P = h.P, Q = h.dev.nq;
+    CK(hipMemcpyAsync(ctx->d_phi + h.dev.q_off, h.prec.data(), Q * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    ows[2 * b] = h.ows_reg_sum;
+    ows[2 * b + 1] = h.ows_num >= 0.f ? h.ows_num : (float)h.widths[h.L - 2];
+    if (step_mode == BANN_STEP_INJECTED) {
+      ep.assign(eps + off, eps + off + P + Q);
+    } else {  // random_step_sizes (654-704): U(0,1) (P + Q)^-1/4 c -- the joint sampler's only mode (1092-1101)
+      ep.resize(P + Q);
+      const float f = powf((float)(P + Q), -0.25f) * factor;
+      for (auto& e : ep) e = U(rng) * f;
+    }
+    CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, ep.data(), P * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipMemcpyAsync(ctx->d_ephi + h.dev.q_off, ep.data() + P, Q * sizeof(float), hipMemcpyHostToDevice,
+                      ctx->stream));
+    if (momentum) {
+      CK(hipMemcpyAsync(ctx->d_mom + h.dev.p_off, momentum + off, P * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+      CK(hipMemcpyAsync(ctx->d_mphi + h.dev.q_off, momentum + off + P, Q * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+    }
+    uu[b] = u ? u[i] : U(rng);
+    off += P + Q;
+    CK(hipStreamSynchronize(ctx->stream));  // ep is reused
+  }
+  CK(hipMemcpyAsync(ctx->d_ows, ows.data(), ows.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_u, uu.data(), uu.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  if (!momentum) {
+    launch_sample_momentum(ctx->st, p.d_all, nb, p.max_p, seed, ctx->stream);
+    launch_sample_momentum_joint(ctx->st, p.d_all, nb, max_q, seed, ctx->stream);
+  }
+  CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
+  rc = run_grad(ctx, p, 0);
+  if (rc) return rc;
+  launch_update_joint(ctx->st, p.d_all, nb, MODE_INIT, 0, ctx->stream);
+  for (int k = 1; k <= L; ++k) {
+    rc = run_grad(ctx, p, 0);
+    if (rc) return rc;
+    launch_update_joint(ctx->st, p.d_all, nb, k < L ? MODE_STEP : MODE_LAST, k, ctx->stream);
+  }
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  const int stride = ctx->htrace_cap;
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
+    BranchHost& h = ctx->br[b];
+    if (status_out) CK(hipMemcpy(status_out + i, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (log_density_out) CK(hipMemcpy(log_density_out + i, ctx->d_ld + b, sizeof(double), hipMemcpyDeviceToHost));
+    if (h_trace_out)
+      CK(hipMemcpy(h_trace_out + (int64_t)i * (L + 1), ctx->d_htrace + (int64_t)b * stride, (L + 1) * sizeof(double),
+                   hipMemcpyDeviceToHost));
+    // the sampled precisions become the branch's precisions (host copy and derived device arrays)
+    CK(hipMemcpy(h.prec.data(), ctx->d_phi + h.dev.q_off, h.dev.nq * sizeof(float), hipMemcpyDeviceToHost));
+    rc = upload_precisions(ctx, b);
+    if (rc) return rc;
+  }
+  return BANN_OK;
+}
+
 extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
                                    int32_t step_mode, float factor, uint64_t seed) {
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is already active (call bann_leapfrog_end)");
   if (!branches || nb <= 0 || L < 1) return fail(ctx, BANN_E_ARG, "bad branch list or L");
   int rc = BANN_OK;
   // the packed launch plan of a branch set is reused across trajectories (a sweep
@@ -1157,6 +1311,8 @@ extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* nu
     int rc = bann_leapfrog_steps(ctx, ctx->lf_L - ctx->lf_step);
     if (rc) return rc;
   }
+  // rejected branches were restored to theta_0: their prediction rows go back to f(theta_0)
+  launch_restore_pred(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->stream);
   CK(hipMemcpyAsync(ctx->h_status, ctx->d_status, ctx->br.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
                     ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
@@ -1196,6 +1352,7 @@ extern "C" int bann_leapfrog_residual_delta(bann_ctx* ctx, float* out_host) {
 
 extern "C" int bann_leapfrog_predictions_device(bann_ctx* ctx, float** out) {
   if (!ctx || !out) return BANN_E_ARG;
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "predictions are current after bann_leapfrog_end");
   *out = ctx->d_pred;
   return BANN_OK;
 }

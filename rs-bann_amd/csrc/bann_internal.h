@@ -43,6 +43,11 @@ struct BranchDev {
   int32_t scr_a[BANN_MAXL];   //   a_l
   int32_t scr_d[BANN_MAXL];   //   delta_l
   int32_t scr_stride;         //   floats per individual
+  // precision coordinates (precision_vec order, params.rs:272-289) for joint HMC
+  int64_t q_off;              // offset into the per-precision arrays (phi, ...)
+  int32_t nq;                 // num precisions
+  int32_t qoff[BANN_MAXL];    // first weight precision of layer l
+  int32_t qbias;              // first bias precision (L-1 of them), then the error precision
 };
 
 // One work item of the fused gradient kernel: a contiguous fragment range of one branch.
@@ -93,6 +98,16 @@ struct DevState {
   int32_t lint;           // trajectory length L (for the trace stride)
   float max_dh;
   unsigned long long* dbg;  // diagnostic phase stamps (BANN_STAMPS=1 with a BANN_ABLATE=16 build), else null
+  // joint HMC (precisions as coordinates, branch_sampler.rs:1070-1178)
+  float* phi;             // precision coordinates [sum nq]
+  float* phi0;            // trajectory start
+  float* mphi;            // their momenta
+  float* ephi;            // their step sizes
+  float* gphi;            // their log-density gradient
+  const int32_t* pidx;    // [sum P]: precision index (within the branch) of every parameter
+  const float* ows;       // [nbranch][2]: output-weight summary stat of the OTHER branches (reg_sum), and
+                          //   the network's output-weight count (OutputWeightSummaryStats, params.rs:404-465)
+  float hyper[6];         // NetworkPrecisionHyperparameters: (shape, scale) dense, summary, output (params.rs:134-142)
 };
 
 // ---- launchers (defined in the kernel translation units) ----
@@ -113,6 +128,11 @@ bool update_is_large(const BranchDev& d);  // served by the 1024-thread update k
 void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_sample_momentum(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, uint64_t seed,
                             hipStream_t s);
+void launch_update_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
+                         hipStream_t s);
+void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_q,
+                                  uint64_t seed, hipStream_t s);
+#define BANN_JOINT_MAXQ 4608  // joint HMC: precisions per branch (ARD: m + hidden widths + L)
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
@@ -126,6 +146,7 @@ void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, 
                             int32_t nchunks, int32_t ntile, hipStream_t s);
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
                        int izmailov, float c, int32_t L, hipStream_t s);
+void launch_restore_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 int64_t residual_delta_scratch_floats(int64_t n);
 void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* scratch, float* out,

@@ -16,6 +16,8 @@
 // combined here in a fixed order (deterministic).
 #include <math.h>
 
+#include <algorithm>
+
 #include "bann_internal.h"
 #include "rng.h"
 
@@ -587,6 +589,20 @@ void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t 
   hipLaunchKernelGGL(k_residual_delta_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, scratch, st.n, out);
 }
 
+// pred <- pred0 for the listed branches that were not accepted (session end)
+__global__ void __launch_bounds__(256) k_restore_pred(DevState st, const int32_t* __restrict__ blist) {
+  const int b = blist[blockIdx.y];
+  if (st.status[b] == ST_ACCEPTED) return;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int64_t r = i; r < st.n; r += (int64_t)gridDim.x * 256) st.pred[(int64_t)b * st.n + r] = st.pred0[(int64_t)b * st.n + r];
+}
+
+void launch_restore_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s) {
+  if (nb <= 0) return;
+  const int64_t blocks = std::min<int64_t>((st.n + 255) / 256, 64);
+  hipLaunchKernelGGL(k_restore_pred, dim3((unsigned)blocks, (unsigned)nb), dim3(256), 0, s, st, branches);
+}
+
 // pred0 <- pred for the listed branches (trajectory start), one launch
 __global__ void __launch_bounds__(256) k_snapshot_pred(DevState st, const int32_t* __restrict__ blist) {
   const int b = blist[blockIdx.y];
@@ -626,4 +642,248 @@ void launch_step_sizes(const DevState& st, const double* base, const int32_t* br
   if (nb <= 0 || max_p <= 0) return;
   hipLaunchKernelGGL(k_step_sizes, dim3((unsigned)((max_p + 255) / 256), (unsigned)nb), dim3(256), 0, s, st, base,
                      branches, izmailov, c, L);
+}
+
+// ===========================================================================
+// joint HMC update: hmc_step_joint (branch_sampler.rs:1070-1178) samples the
+// parameters AND the precisions.  Per branch and leapfrog step (one workgroup):
+//   * per-precision statistics S_q of the current theta: sum theta^2 (ridge) or
+//     sum |theta| (lasso) over each precision's group -- an ARD row (one thread,
+//     fixed order), a whole layer or a bias vector (fixed-order block sums);
+//   * log_density_gradient_joint (406-422): the parameter gradient with the
+//     precisions taken from the coordinates phi (l2-regularised biases,
+//     333-344), the precision gradients (ridge_ard.rs:221-250, lasso_ard.rs,
+//     ridge_base.rs, lasso_base.rs; bias precisions 346-367, error precision
+//     369-378);
+//   * the joint -H (log_density_joint 292-305 with the output-weight term of the
+//     other branches, minus K over both momenta, momentum.rs:78-101), early
+//     rejection on it, and the Metropolis test of accept_or_reject_hmc_state
+//     (928-962), whose final -H uses the NON-joint log_density (72-78) -- a
+//     reference quirk kept for parity;
+//   * momentum half steps and the position steps of both coordinate sets
+//     (params.rs:344-355, 728-738).
+// ===========================================================================
+#define UPD_J 256
+
+// (shape, scale) of layer l: NetworkPrecisionHyperparameters::layer_prior_hyperparams (params.rs:146-163)
+__device__ __forceinline__ void hyper_of(const DevState& st, int l, int L, double& k, double& s) {
+  const int c = l == L - 1 ? 2 : (l == L - 2 ? 1 : 0);
+  k = (double)st.hyper[2 * c];
+  s = (double)st.hyper[2 * c + 1];
+}
+
+__global__ void __launch_bounds__(UPD_J) k_update_joint(DevState st, const int32_t* __restrict__ blist, int mode,
+                                                        int step) {
+  __shared__ double s_S[BANN_JOINT_MAXQ];
+  __shared__ double redd[4 * (UPD_J / 64)];
+  const int b = blist[blockIdx.x];
+  const BranchDev bd = st.br[b];
+  const int P = bd.P, nq = bd.nq, L = bd.L, t = threadIdx.x;
+  const int64_t base = bd.p_off, qb = bd.q_off;
+  if ((mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
+  const bool lasso = bd.prior == 2 || bd.prior == 3;
+  const bool ard = bd.prior == 0 || bd.prior == 2;
+  double rss = 0.0;
+  for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
+  float* phi = st.phi + qb;
+  const float le = phi[nq - 1];
+  const double n = (double)st.n;
+
+  // ---- S_q at the current theta ----
+  for (int q = t; q < nq; q += UPD_J) s_S[q] = 0.0;
+  __syncthreads();
+  for (int l = 0; l < L; ++l) {
+    const int wi = bd.win[l], wo = bd.widths[l];
+    const float* W = st.theta + base + bd.woff[l];
+    if (ard && l < L - 1) {  // one precision per input row, tiled over the columns (ridge_ard.rs:36-37)
+      for (int j = t; j < wi; j += UPD_J) {
+        double a = 0.0;
+        for (int k = 0; k < wo; ++k) {
+          const double w = (double)W[k * wi + j];
+          a += lasso ? fabs(w) : w * w;
+        }
+        s_S[bd.qoff[l] + j] = a;
+      }
+    } else {
+      double a[1] = {0.0};
+      for (int i = t; i < wi * wo; i += UPD_J) {
+        const double w = (double)W[i];
+        a[0] += lasso ? fabs(w) : w * w;
+      }
+      block_sum_n<UPD_J, 1>(a, redd);
+      if (t == 0) s_S[bd.qoff[l]] = a[0];
+    }
+  }
+  for (int l = 0; l < L - 1; ++l) {  // bias precisions: l2 (sum_of_squares, 346-367)
+    const float* B = st.theta + base + bd.boff[l];
+    double a[1] = {0.0};
+    for (int i = t; i < bd.widths[l]; i += UPD_J) a[0] += (double)B[i] * (double)B[i];
+    block_sum_n<UPD_J, 1>(a, redd);
+    if (t == 0) s_S[bd.qbias + l] = a[0];
+  }
+  __syncthreads();
+
+  // sums[0]: joint log density (every term is attached to one precision),
+  // sums[1]: sum p^2 over both momenta, sums[2]: non-joint weight prior
+  double sums[3] = {0.0, 0.0, 0.0};
+  for (int i = t; i < P; i += UPD_J) {
+    float d = 0.f;
+    for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
+    const float th = st.theta[base + i];
+    const float lm = phi[st.pidx[base + i]];
+    float reg;
+    if (i >= bd.boff[0])
+      reg = lm * th;  // log_density_gradient_wrt_biases_l2 (333-344)
+    else
+      reg = lasso ? lm * (th > 0.f ? 1.f : (th < 0.f ? -1.f : 0.f)) : lm * th;
+    const float gr = -(le * d + reg);
+    st.grad[base + i] = gr;
+    float p = st.mom[base + i];
+    if (mode != MODE_INIT) {  // second half step of this leapfrog step (momentum.rs:30-63)
+      p = p + st.eps[base + i] * 0.5f * gr;
+      st.mom[base + i] = p;
+    }
+    sums[1] += (double)p * (double)p;
+  }
+  for (int q = t; q < nq; q += UPD_J) {
+    const double lam = (double)phi[q], S = s_S[q];
+    double k, s, g, ldj, ldn = 0.0;
+    if (q == nq - 1) {  // error precision (log_density_joint_wrt_rss 240-257, gradient 369-378)
+      hyper_of(st, L - 1, L, k, s);
+      g = (2.0 * k + n - 2.0) / (2.0 * lam) - 1.0 / s - rss / 2.0;
+      ldj = (k + (n - 2.0) / 2.0) * log(lam) - lam * (rss / 2.0 + 1.0 / s);
+    } else if (q >= bd.qbias) {  // bias precision (260-279, 346-367)
+      const int l = q - bd.qbias;
+      hyper_of(st, l, L, k, s);
+      const double nv = (double)bd.widths[l];
+      g = (2.0 * k + (nv - 2.0)) / (2.0 * lam) - 1.0 / s - S / 2.0;
+      ldj = -lam * (S / 2.0 + 1.0 / s) + (k + (nv - 2.0) / 2.0) * log(lam);
+    } else {
+      int l = 0;
+      while (l + 1 < L && bd.qoff[l + 1] <= q) ++l;
+      hyper_of(st, l, L, k, s);
+      if (l == L - 1) {  // output layer: the other branches' summary stat joins (ridge_ard.rs:150-169, 236-248)
+        const double rs = (double)st.ows[2 * b], np_ = (double)st.ows[2 * b + 1];
+        if (lasso) {
+          g = (k + np_ - 1.0) / lam - 1.0 / s - (S + rs);
+          ldj = -((S + rs) + 1.0 / s) * lam + (k + np_ - 1.0) * log(lam);
+        } else {
+          g = (2.0 * k + np_ - 2.0) / (2.0 * lam) - 1.0 / s - (S + rs) / 2.0;
+          ldj = -(0.5 * (S + rs) + 1.0 / s) * lam + (k + (np_ - 2.0) / 2.0) * log(lam);
+        }
+      } else if (ard) {  // per input row: the gradient counts the rows (precisions.elements(), quirk), the density the columns
+        const double nr = (double)bd.win[l], nc = (double)bd.widths[l];
+        if (lasso) {
+          g = (k + nr - 1.0) / lam - 1.0 / s - S;
+          ldj = -(S + 1.0 / s) * lam + (k + nc - 1.0) * log(lam);
+        } else {
+          g = (2.0 * k + nr - 2.0) / (2.0 * lam) - 1.0 / s - S / 2.0;
+          ldj = -(S / 2.0 + 1.0 / s) * lam + (k + (nc - 2.0) / 2.0) * log(lam);
+        }
+      } else {  // base priors: one precision per layer
+        const double sz = (double)bd.win[l] * (double)bd.widths[l];
+        if (lasso) {
+          g = (k + sz - 1.0) / lam - 1.0 / s - S;
+          ldj = -(S + 1.0 / s) * lam + (k + sz - 1.0) * log(lam);
+        } else {
+          g = (2.0 * k + sz - 2.0) / (2.0 * lam) - 1.0 / s - S / 2.0;
+          ldj = -(S / 2.0 + 1.0 / s) * lam + (k + (sz - 2.0) / 2.0) * log(lam);
+        }
+      }
+      ldn = -lam * (lasso ? S : S / 2.0);  // non-joint log_density_wrt_weights (ridge_ard.rs:171-194 etc.)
+    }
+    const float gq = (float)g;
+    st.gphi[qb + q] = gq;
+    float p = st.mphi[qb + q];
+    if (mode != MODE_INIT) {
+      p = p + st.ephi[qb + q] * 0.5f * gq;
+      st.mphi[qb + q] = p;
+    }
+    sums[0] += ldj;
+    sums[1] += (double)p * (double)p;
+    sums[2] += ldn;
+  }
+  block_sum_n<UPD_J, 3>(sums, redd);
+  const double ldj = sums[0];
+  const double ldn = sums[2] - (double)le * rss / 2.0;
+  const double h = ldj - 0.5 * sums[1];
+  const int stride = st.lint + 1;
+  int act = 0;  // 0: (half step +) position step, 1: restore theta0 / phi0, 2: keep
+  if (mode == MODE_INIT) {
+    if (t == 0) {
+      st.h0[b] = h;
+      st.htrace[(int64_t)b * stride] = h;
+      st.status[b] = ST_RUNNING;
+      st.uturn[b] = -1;
+      st.rss_out[b] = rss;
+      st.ld_out[b] = ldn;
+    }
+  } else {
+    const double h0 = st.h0[b];
+    if (t == 0) st.htrace[(int64_t)b * stride + step] = h;
+    if (fabs(h - h0) > (double)st.max_dh) {  // RejectedEarly (1138-1158); NaN never exceeds
+      act = 1;
+      if (t == 0) st.status[b] = ST_REJECTED_EARLY;
+    } else if (mode == MODE_LAST) {  // accept_or_reject_hmc_state: the final -H is NON-joint (943)
+      const double log_acc = (ldn - 0.5 * sums[1]) - h0;
+      const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
+      const bool accept = (double)st.uacc[b] < acc_p;
+      act = accept ? 2 : 1;
+      if (t == 0) {
+        st.status[b] = accept ? ST_ACCEPTED : ST_REJECTED;
+        st.ld_out[b] = ldn;
+        st.rss_out[b] = rss;
+      }
+    }
+  }
+  if (act == 0) {
+    for (int i = t; i < P; i += UPD_J) {
+      const float e = st.eps[base + i], th = st.theta[base + i];
+      const float p = st.mom[base + i] + 0.5f * e * st.grad[base + i];
+      st.mom[base + i] = p;
+      if (mode == MODE_INIT) st.theta0[base + i] = th;
+      st.theta[base + i] = th + e * p;
+    }
+    for (int q = t; q < nq; q += UPD_J) {
+      const float e = st.ephi[qb + q], v = phi[q];
+      const float p = st.mphi[qb + q] + 0.5f * e * st.gphi[qb + q];
+      st.mphi[qb + q] = p;
+      if (mode == MODE_INIT) st.phi0[qb + q] = v;
+      phi[q] = v + e * p;
+    }
+  } else if (act == 1) {
+    for (int i = t; i < P; i += UPD_J) st.theta[base + i] = st.theta0[base + i];
+    for (int q = t; q < nq; q += UPD_J) phi[q] = st.phi0[qb + q];
+  }
+  if (bd.fused && act != 2) {
+    __syncthreads();
+    refresh_fused_const<UPD_J>(st, b, bd);
+  }
+}
+
+void launch_update_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
+                         hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_update_joint, dim3(nb), dim3(UPD_J), 0, s, st, branches, mode, step);
+}
+
+// N(0, 1) momenta of the precision coordinates (sample_joint_momentum, 611-645)
+__global__ void k_sample_momentum_phi(DevState st, const int32_t* __restrict__ blist, uint64_t seed) {
+  const int b = blist[blockIdx.y];
+  const BranchDev bd = st.br[b];
+  const int i2 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * i2 >= bd.nq) return;
+  const u32x4 r = philox_bits(seed, 0x7A0E100ull + (uint64_t)b, (uint64_t)i2);
+  const float rad = sqrtf(-2.f * logf(u01_open(r.x)));
+  float sn, cs;
+  sincosf(6.283185307179586f * u01(r.y), &sn, &cs);
+  st.mphi[bd.q_off + 2 * i2] = rad * cs;
+  if (2 * i2 + 1 < bd.nq) st.mphi[bd.q_off + 2 * i2 + 1] = rad * sn;
+}
+
+void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_q,
+                                  uint64_t seed, hipStream_t s) {
+  if (nb <= 0 || max_q <= 0) return;
+  const int pairs = (max_q + 1) / 2;
+  hipLaunchKernelGGL(k_sample_momentum_phi, dim3((pairs + 255) / 256, nb), dim3(256), 0, s, st, branches, seed);
 }

@@ -612,3 +612,66 @@ def test_c5_shape_wide_full_n(Ctx):
     assert norm_rel(grad, O.param_vec(ogw, ogb)) < 3e-2
     assert scalar_close(rss, orss, 1e-2)
     ctx.close()
+
+
+# ------------------------------------------------------------ joint HMC parity
+HYPER = (0.5, 2.0, 0.8, 3.0, 1.1, 5.0)   # dense, summary, output (shape, scale)
+
+
+@pytest.mark.parametrize("shape", [("fx", 60, [4, 4, 1]), ("wide", 40, [8, 8, 1]), ("generic", 30, [6, 5, 3, 1])])
+@pytest.mark.parametrize("prior", ["ridge_ard", "ridge_base", "lasso_ard", "lasso_base"])
+def test_hmc_step_joint_parity(Ctx, prior, shape):
+    """hmc_step_joint (branch_sampler.rs:1070-1178) with injected step sizes,
+    momenta and uniform: the joint -H trace (parameter and precision gradients,
+    joint log density incl. the other branches' output-weight stat), the status
+    (final test on the NON-joint density, the reference quirk), the final
+    parameters and the sampled precisions match the oracle."""
+    path, m, widths = shape
+    rng = np.random.default_rng(31)
+    n, L = 500, 6
+    g = O.synthetic_genotypes(rng, n, m)
+    br = f32_branch(O.random_branch(rng, m, widths, prior=prior, act="tanh"))
+    br.out_reg_sum, br.out_num_params = float(np.float32(0.37)), 24.0
+    ctx = build_context(Ctx, g, [dict(snps=np.arange(m, dtype=np.int32), branch=br, y=np.zeros(n))])
+    assert ctx.kernel_path(0) == {"fx": "fused", "wide": "wide", "generic": "generic"}[path]
+    ctx.set_output_stats(0, br.out_reg_sum, br.out_num_params)
+    X = oracle_inputs(ctx, g, np.arange(m))
+    y = (O.predict(br, X) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    P, Q = br.num_params, O.precision_vec(br).size
+    hp = O.Hyper(dense=HYPER[0:2], summary=HYPER[2:4], output=HYPER[4:6])
+    for u, scale in [(0.3, 2e-4), (0.3, 3e-3), (0.5, 1.0)]:   # small, larger, absurd (early rejection)
+        eps = (scale * rng.uniform(size=P + Q)).astype(np.float32)
+        p0 = rng.normal(size=P + Q).astype(np.float32)
+        theta0 = ctx.get_params(0)
+        res = ctx.hmc_step_joint([0], L, HYPER, eps=eps, momentum=p0, u=[u])
+        ob = br.copy()
+        out = O.hmc_step_joint(ob, X, y, hp, eps.astype(np.float64), p0.astype(np.float64), L, 10.0, u)
+        assert res["status"][0] == out["status"], (scale, res["status"], out["status"])
+        tr = np.asarray(out["trace"])
+        gt = res["trace"][0][: tr.size]
+        # a diverged step's -H (|dH| ~ 1e10 at scale 1) is f32 noise vs float64: check the status only there
+        fin = np.isfinite(tr) & (np.abs(tr - tr[0]) <= 10.0)
+        assert np.all(np.abs(gt[fin] - tr[fin]) <= 1e-5 * np.maximum(1.0, np.abs(tr[fin]))), (scale, gt, tr)
+        assert norm_rel(ctx.get_params(0), O.param_vec(ob.weights, ob.biases)) < 1e-5
+        assert norm_rel(ctx.get_precisions(0), O.precision_vec(ob)) < 1e-5
+        if out["status"] != O.REJECTED_EARLY:
+            assert scalar_close(res["log_density"][0], out["log_density"]), (res["log_density"], out["log_density"])
+        if out["status"] != O.ACCEPTED:
+            assert np.array_equal(ctx.get_params(0), theta0)
+        br = ob
+    ctx.close()
+
+
+def test_hmc_step_joint_refuses_std_normal_and_reports_shapes(Ctx):
+    rng = np.random.default_rng(3)
+    n, m = 100, 20
+    g = O.synthetic_genotypes(rng, n, m)
+    br = f32_branch(O.random_branch(rng, m, [4, 1], prior="std_normal"))
+    ctx = build_context(Ctx, g, [dict(snps=np.arange(m), branch=br, y=np.zeros(n))])
+    from bann import BannError
+    with pytest.raises(BannError):
+        ctx.hmc_step_joint([0], 3, HYPER)
+    with pytest.raises(ValueError):   # eps must cover parameters AND precisions
+        ctx.hmc_step_joint([0], 3, HYPER, eps=np.ones(br.num_params, np.float32))
+    ctx.close()
