@@ -102,6 +102,10 @@ def main():
                     help="profiling only: run rank 0's shard of an N-GPU job on this one GPU, no collective")
     ap.add_argument("--hidden-bf16", action="store_true",
                     help="wide kernel: hidden GEMMs on bf16 MFMA (C5's bf16 vs fp32 comparison)")
+    ap.add_argument("--sampler", default="branch", choices=["branch", "network"],
+                    help="branch: every branch's trajectory against the sweep-start residual, one residual "
+                         "exchange per trajectory (default); network: one HMC state over all branches, the summed "
+                         "branch outputs all-reduced every leapfrog step (bann_network_hmc_step)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,7 +123,7 @@ def main():
         dist = dist_mod
 
     from bann import BannContext
-    from bann.distributed import allreduce_sum_, shard_ranges
+    from bann.distributed import TorchAllreduce, comm_unique_id, shard_ranges
 
     n, M_total, B_total, widths = CONFIGS[args.config]
     if args.step_factor is None:
@@ -177,31 +181,39 @@ def main():
     ctx.synchronize()
     setup_s = time.time() - t_setup
 
-    delta = None
-    if dist is not None:   # initialise torch/HIP state before the timed region
+    # the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
+    # all-reduce callback when rehearsing N ranks on one GPU
+    if dist is not None:
         import torch
-        delta = torch.zeros(n, dtype=torch.float32, device=f"cuda:{local_rank}")
+        if backend == "nccl":
+            idt = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local_rank}")
+            if rank == 0:
+                idt.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(idt, 0)
+            ctx.comm_init_rccl(bytes(idt.cpu().numpy()), world, rank)
+        else:
+            ctx.comm_callback(TorchAllreduce(dist), world, rank)
         torch.cuda.synchronize()
     branches = list(range(nb))
+    residual = noise.astype(np.float32)   # the sweep's residual y - sum_b f_b (net.rs:279-300)
+    y_net = (noise + fsum).astype(np.float32)
 
     def trajectory(L, seed):
-        """one HMC trajectory of L leapfrog steps for every branch of this rank:
-        momentum draw + initial gradient, L fused steps, Metropolis, and the
-        residual change of the accepted branches (all-reduced over ranks)."""
+        """one HMC trajectory of L leapfrog steps.  branch sampler: every branch of
+        this rank (momentum draw + initial gradient, L fused steps, Metropolis),
+        then the residual change of the accepted branches exchanged over the ranks
+        inside the library (bann_exchange_residual).  network sampler: one HMC
+        state over all branches of all ranks, the summed outputs all-reduced every
+        step (bann_network_hmc_step)."""
+        nonlocal residual
+        if args.sampler == "network":
+            r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov",
+                                     step_factor=args.step_factor, seed=seed, u=0.5)
+            return float(r["status"] == 0) * nb
         ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
         ctx.leapfrog_steps(L)
         status, acc = ctx.leapfrog_end()
-        if dist is not None:
-            ctx.residual_delta_device(delta.data_ptr())
-            if backend == "nccl":
-                allreduce_sum_(delta, dist)   # RCCL over xGMI: the sweep-level residual exchange
-            else:
-                dc = delta.cpu()
-                allreduce_sum_(dc, dist)
-                delta.copy_(dc)
-            torch.cuda.synchronize()
-        else:   # one GPU: no torch in the process (rocprofv3 + torch's HIP runtime do not mix here)
-            ctx.residual_delta()
+        residual = ctx.exchange_residual(residual)
         return acc
 
     # warmup: a full trajectory of W steps (loads every kernel, ramps the clocks)
@@ -215,6 +227,7 @@ def main():
     acc = trajectory(args.steps, seed=11 + rank)   # timed: one whole trajectory of K steps
     ctx.synchronize()
     if dist is not None:
+        torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -228,7 +241,8 @@ def main():
         acc_all, nb_all = float(acc), float(nb)
 
     workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
-                "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else ""))
+                "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else "") +
+                (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else ""))
     kernel_name = "k_fused_grad_wx" if wide else ("k_fused_grad_fx" if m_b <= 512 else "k_fused_grad_fxl")
     # ---- kernel timing for the roofline (HIP events on the library stream) ----
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)

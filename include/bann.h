@@ -224,6 +224,54 @@ int bann_synchronize(bann_ctx* ctx);
  * average milliseconds per launch of each. */
 int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms);
 
+/* ---------------- multi-GPU: branch shards, one process (rank) per GPU ----------------
+ * Branches share no weights: a rank owns a contiguous branch
+ * range and only its markers' genotypes.  The context's communicator carries
+ * the two exchanges of the path: the per-trajectory residual change of a
+ * leapfrog session (the sweep bookkeeping of net.rs:292-300, over ranks) and,
+ * in network-joint HMC, the per-step sum of the branch outputs.  The reference
+ * is single-device (no collectives); these entry points have no counterpart. */
+
+/* in-place sum over ranks of count values (dtype 0 = f32, 1 = f64) in a HOST
+ * buffer, e.g. MPI_Allreduce or a gloo all_reduce; returns 0 on success */
+typedef int (*bann_allreduce_fn)(void* user, void* host_buf, int64_t count, int32_t dtype);
+
+/* contiguous branch ranges with ~equal marker totals: rank r owns
+ * [starts_out[r], starts_out[r+1]); starts_out has world+1 entries; world must
+ * not exceed nbranches (every rank owns a branch).  Host only. */
+int bann_shard_branches(const int32_t* marker_counts, int32_t nbranches, int32_t world, int32_t* starts_out);
+/* RCCL (xGMI) communicator: rank 0 calls bann_comm_unique_id, every rank gets
+ * the 128 bytes out of band, then all ranks call bann_ctx_comm_init together */
+int bann_comm_unique_id(uint8_t* id_out);
+int bann_ctx_comm_init(bann_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank);
+/* a caller-provided all-reduce on host buffers instead of RCCL */
+int bann_ctx_comm_callback(bann_ctx* ctx, bann_allreduce_fn fn, void* user, int32_t nranks, int32_t rank);
+/* residual bookkeeping over ranks on the host: local_delta is summed over the
+ * ranks in place, then residual[i] -= local_delta[i].  The exchange step of
+ * bann_exchange_residual for a callback communicator.  Host only. */
+int bann_residual_update_host(bann_allreduce_fn fn, void* user, float* local_delta, float* residual, int64_t n);
+/* after bann_leapfrog_end: residual_host[i] -= (sum over ranks of each rank's
+ * bann_leapfrog_residual_delta)[i]; collective over the ranks */
+int bann_exchange_residual(bann_ctx* ctx, float* residual_host);
+/* network-joint HMC trajectory (SURVEY 8(e) packed-joint mode): the parameters
+ * of every branch of every rank form ONE HMC state for
+ *   -U = -lambda_e/2 ||sum_b f_b + bias - y||^2 + sum_b log prior_b(theta_b)
+ * Per leapfrog step: a forward launch over the local branches, ONE all-reduce
+ * of the n-vector sum of their outputs, e = sum f + bias - y as every branch's
+ * output error (the summary output and its gradient), a gradient launch and
+ * the update.  -H is summed over the ranks; early rejection and the Metropolis
+ * test (u) decide for the whole network, identically on every rank.  Collective.
+ *   y: n targets on the host (identical on every rank); step_mode: Izmailov or
+ *   uniform (device step sizes from the local precisions) or INJECTED (eps:
+ *   the local branches' step sizes, concatenated in branch order); momentum:
+ *   concatenated p0 of the local branches or NULL (device N(0,1) from seed; a
+ *   rank-distinct stream is the caller's choice of seed); u: the uniform.
+ * Outputs (may be NULL): status, h_trace[L+1], rss of the final state. */
+int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
+                          float max_hamiltonian_error, int32_t step_mode, float step_factor, const float* eps,
+                          const float* momentum, uint64_t seed, float u, int32_t* status_out, double* h_trace_out,
+                          double* rss_out);
+
 /* ---------------- introspection for tests / profiling ---------------- */
 /* which gradient kernel serves branch b: 1 = fx fused single-pass kernel (every
  * width <= 4, m <= 512), 3 = fxl (every width <= 4, 512 < m <= 4096: one wave

@@ -643,6 +643,67 @@ def hmc_step_joint(br: Branch, X, y, hp: Hyper, eps, p, L_int: int, max_dH: floa
 
 
 # --------------------------------------------------------------------------
+# network-joint HMC (bann_network_hmc_step; SURVEY 8(e) packed-joint mode)
+# --------------------------------------------------------------------------
+def network_hmc_step(brs: Sequence[Branch], Xs, y, bias: float, lambda_e: float, eps_list, p_list, L_int: int,
+                     max_dH: float, u: float):
+    """One HMC state over the parameters of every branch:
+        -U = -lambda_e/2 ||sum_b f_b + bias - y||^2 + sum_b log prior_b
+    (log prior_b = log_density(b, rss = 0): the branch's own prior terms,
+    branch_sampler.rs:72-78 / std_normal_branch.rs:149-158).  The gradient of
+    branch b is its backpropagate (813-875) against the target f_b - e, e the
+    network error, i.e. J_b^T e.  Leapfrog as hmc_step (1239-1262), one
+    Metropolis decision for the network; a divergence at any step rejects
+    early.  eps_list / p_list: per-branch param_vec-ordered vectors.  Branches
+    are updated in place (restored on rejection)."""
+    brs = list(brs)
+    for b in brs:
+        b.error_precision = lambda_e
+    init = [b.copy() for b in brs]
+    eps = [np.asarray(e, dtype=np.float64) for e in eps_list]
+    p = [np.array(x, dtype=np.float64) for x in p_list]
+
+    def grads():
+        preds = [predict(b, X) for b, X in zip(brs, Xs)]
+        e = sum(preds) + bias - y
+        gs = []
+        for b, X, f in zip(brs, Xs, preds):
+            gw, gb, _ = log_density_gradient(b, X, f - e)
+            gs.append(param_vec(gw, gb))
+        return gs, float(e @ e)
+
+    def neg_h(rss_v):
+        return (sum(log_density(b, 0.0) for b in brs) - lambda_e * rss_v / 2.0
+                - 0.5 * sum(float(q @ q) for q in p))
+
+    g, r = grads()
+    H0 = neg_h(r)
+    trace = [H0]
+    status = ACCEPTED
+    for step in range(L_int):
+        for k, b in enumerate(brs):
+            p[k] += 0.5 * eps[k] * g[k]
+            th = param_vec(b.weights, b.biases) + eps[k] * p[k]
+            b.weights, b.biases = load_param_vec(th, b.num_markers, b.layer_widths)
+        g, r = grads()
+        for k in range(len(brs)):
+            p[k] += 0.5 * eps[k] * g[k]
+        H = neg_h(r)
+        trace.append(H)
+        if abs(H - H0) > max_dH:
+            status = REJECTED_EARLY
+            break
+    if status == ACCEPTED:
+        log_acc = trace[-1] - H0
+        acc_p = 1.0 if log_acc >= 0 else math.exp(log_acc)
+        status = ACCEPTED if u < acc_p else REJECTED
+    if status != ACCEPTED:
+        for b, b0 in zip(brs, init):
+            b.weights, b.biases = b0.weights, b0.biases
+    return dict(status=status, trace=trace, rss=r)
+
+
+# --------------------------------------------------------------------------
 # Gibbs precision posteriors (host side): gibbs_steps.rs, ridge_ard.rs:271-301
 # --------------------------------------------------------------------------
 def ridge_posterior_params(shape: float, scale: float, sum_sq: float, num: int):

@@ -55,6 +55,8 @@ class McmcCfg(C.Structure):
                 ("sampled_output_bias", C.c_int32)]
 
 
+# bann_allreduce_fn: in-place sum over ranks of a host buffer (dtype 0 f32, 1 f64)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32)
 UNIFORM_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
 NORMAL_FN = C.CFUNCTYPE(C.c_double, C.c_void_p)
 GAMMA_FN = C.CFUNCTYPE(C.c_double, C.c_void_p, C.c_double, C.c_double)
@@ -107,6 +109,14 @@ SIGNATURES = {
     "bann_hmc_step_joint": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pf32,
                                       _pi32, _pf64, _pf64]),
     "bann_branch_set_output_stats": (C.c_int, [_P, _i32, _f32, _f32]),
+    "bann_shard_branches": (C.c_int, [_pi32, _i32, _i32, _pi32]),
+    "bann_comm_unique_id": (C.c_int, [_pu8]),
+    "bann_ctx_comm_init": (C.c_int, [_P, _pu8, _i32, _i32]),
+    "bann_ctx_comm_callback": (C.c_int, [_P, ALLREDUCE_FN, _P, _i32, _i32]),
+    "bann_residual_update_host": (C.c_int, [ALLREDUCE_FN, _P, _pf32, _pf32, _i64]),
+    "bann_exchange_residual": (C.c_int, [_P, _pf32]),
+    "bann_network_hmc_step": (C.c_int, [_P, _pf32, _f32, _f32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _f32,
+                                        _pi32, _pf64, _pf64]),
     "bann_leapfrog_begin": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _u64]),
     "bann_leapfrog_steps": (C.c_int, [_P, _i32]),
     "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),

@@ -280,6 +280,47 @@ class BannContext:
             _ptr(status, C.c_int32), _ptr(trace, C.c_double), _ptr(ld, C.c_double)))
         return dict(status=status, trace=trace, log_density=ld)
 
+    # ------------------------------------------------------ multi-GPU
+    def comm_init_rccl(self, unique_id: bytes, nranks: int, rank: int):
+        """RCCL communicator (collective: every rank calls it with rank 0's id)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self._lib.bann_ctx_comm_init(self._h, buf, nranks, rank))
+
+    def comm_callback(self, allreduce, nranks: int, rank: int):
+        """caller all-reduce (bann.distributed.TorchAllreduce) instead of RCCL."""
+        self._allreduce = allreduce   # the library keeps the function pointer
+        self._check(self._lib.bann_ctx_comm_callback(self._h, allreduce.fn, None, nranks, rank))
+
+    def exchange_residual(self, residual) -> np.ndarray:
+        """residual -= sum over ranks of the last session's residual change (collective)."""
+        res = np.ascontiguousarray(residual, dtype=np.float32).copy()
+        self._check(self._lib.bann_exchange_residual(self._h, _ptr(res, C.c_float)))
+        return res
+
+    def network_hmc_step(self, y, L: int, bias: float = 0.0, lambda_e: float = 1.0,
+                         max_hamiltonian_error: float = 10.0, step_mode: str = "izmailov",
+                         step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0, u: float = 0.5):
+        """network-joint HMC trajectory over every branch of every rank (collective).
+        eps / momentum: concatenated over this context's branches in branch order (or None)."""
+        ya = _f32(y)
+        if ya.size != self.n:
+            raise ValueError(f"y has {ya.size} entries, n = {self.n}")
+        br = np.arange(self.num_branches, dtype=np.int32)
+        eps_a = _f32(eps) if eps is not None else None
+        mom_a = _f32(momentum) if momentum is not None else None
+        self._check_sizes(br, eps_a, mom_a, None)
+        mode = STEP_MODES["injected"] if eps is not None else STEP_MODES[step_mode]
+        nullf = C.POINTER(C.c_float)()
+        st = C.c_int32()
+        tr = np.zeros(L + 1, np.float64)
+        rss = C.c_double()
+        self._check(self._lib.bann_network_hmc_step(
+            self._h, _ptr(ya, C.c_float), bias, lambda_e, L, max_hamiltonian_error, mode, step_factor,
+            _ptr(eps_a, C.c_float) if eps_a is not None else nullf,
+            _ptr(mom_a, C.c_float) if mom_a is not None else nullf, seed, u, C.byref(st), _ptr(tr, C.c_double),
+            C.byref(rss)))
+        return dict(status=st.value, trace=tr, rss=rss.value)
+
     # ------------------------------------------------------ leapfrog session
     def leapfrog_begin(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,
                        step_mode: str = "izmailov", step_factor: float = 1.0, seed: int = 0):

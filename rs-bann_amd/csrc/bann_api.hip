@@ -15,124 +15,16 @@
 #include <string>
 #include <vector>
 
-#include "../../include/bann.h"
-#include "bann_internal.h"
+#include "ctx_internal.h"
 
 #define BANN_VERSION "rs-bann_amd 0.1.0 (gfx950, HIP)"
 
-namespace {
-
-struct BranchHost {
-  std::vector<int32_t> snp_idx;
-  std::vector<int32_t> widths;
-  int32_t m = 0, L = 0, act = 0, prior = 0;
-  int32_t P = 0, nprec = 0;
-  std::vector<float> prec;  // precision_vec order
-  float ows_reg_sum = 0.f;  // output-weight summary stat of the OTHER branches (joint HMC)
-  float ows_num = -1.f;     // output-weight count of the network (< 0: this branch's own)
-  BranchDev dev{};
-};
-
-// one packed gradient launch: every work item of one kernel instantiation
-struct LaunchGroup {
-  int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
-  int32_t L = 0, act = 0, nw = 1, full = 0;
-  std::vector<GradItem> items;
-  GradItem* d_items = nullptr;
-};
-
-struct Plan {
-  std::vector<int32_t> all, generic;
-  int32_t n_small = 0, n_large = 0;  // update kernels: d_all[nb .. nb+n_small) small, then n_large large
-  std::vector<LaunchGroup> groups;
-  int32_t max_p_generic = 0, max_p = 0;
-  int32_t* d_all = nullptr;
-  int32_t* d_gen = nullptr;
-  bool owns = false;
-};
-
-}  // namespace
-
-struct bann_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  // genotypes
-  int64_t n = 0, M = 0;
-  int8_t* d_g = nullptr;
-  float* d_mu = nullptr;
-  float* d_sigma = nullptr;
-  // branches
-  std::vector<BranchHost> br;
-  bool finalized = false;
-  bool fused_enabled = true;
-  bool wide_bf16 = false;  // wx kernel: hidden GEMMs on bf16 MFMA (opt-in, reduced precision)
-  int32_t nfrag = 0, max_splits = 1;
-  int64_t packed_bytes = 0, total_p = 0;
-  // device buffers
-  BranchDev* d_br = nullptr;
-  uint8_t* d_xu2 = nullptr;  // 2-bit genotype tile images of every branch (u2t, kernels_fx.hip)
-  uint8_t* d_dig = nullptr;
-  FusedConst* d_fc = nullptr;
-  float *d_mub = nullptr, *d_sigb = nullptr;
-  float *d_theta = nullptr, *d_mom = nullptr, *d_eps = nullptr, *d_theta0 = nullptr, *d_lam = nullptr,
-        *d_lamld = nullptr, *d_grad = nullptr, *d_part = nullptr;
-  double* d_rss_part = nullptr;
-  float* d_pred0 = nullptr;
-  double* d_stepbase = nullptr;  // per-parameter Izmailov step base (sign: factor applies)
-  float *d_phi = nullptr, *d_phi0 = nullptr, *d_mphi = nullptr, *d_ephi = nullptr, *d_gphi = nullptr;  // joint HMC
-  int32_t* d_pidx = nullptr;
-  float* d_ows = nullptr;
-  int64_t total_q = 0;
-  float* d_delta = nullptr;       // n floats: residual change of the last trajectory (host-copy variant)
-  float* d_delta_part = nullptr;  // per-branch-slice partial rows of the residual change
-  int32_t* h_status = nullptr;    // pinned host mirrors (trajectory status, residual change)
-  float* h_delta = nullptr;
-  float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
-  double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
-  int32_t *d_status = nullptr, *d_uturn = nullptr;
-  int32_t htrace_cap = 0;  // L+1 capacity of d_htrace rows
-  // scratch plan buffers (per-call plans)
-  int32_t* d_list_scr = nullptr;
-  int32_t* d_gen_scr = nullptr;
-  GradItem* d_items_scr = nullptr;
-  unsigned long long* d_dbg = nullptr;  // BANN_STAMPS diagnostics
-  int64_t items_cap = 0;
-  // leapfrog session
-  Plan lf;
-  bool lf_active = false;
-  int32_t lf_L = 0, lf_step = 0;
-  DevState st{};
-};
+void comm_destroy(bann_ctx* ctx);  // bann_dist.hip
 
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
-static int fail(bann_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-#define CK(call)                                                                          \
-  do {                                                                                    \
-    hipError_t e_ = (call);                                                               \
-    if (e_ != hipSuccess)                                                                 \
-      return fail(ctx, e_ == hipErrorOutOfMemory ? BANN_E_OOM : BANN_E_HIP,              \
-                  std::string(#call) + ": " + hipGetErrorString(e_));                     \
-  } while (0)
-
-template <typename T>
-static hipError_t dalloc(T** p, int64_t count) {
-  *p = nullptr;
-  if (count <= 0) count = 1;
-  return hipMalloc((void**)p, (size_t)count * sizeof(T));
-}
-
-static void dfree(void* p) {
-  if (p) (void)hipFree(p);
-}
-
-static void free_plan(Plan& p) {
+void free_plan(Plan& p) {
   if (p.owns) {
     dfree(p.d_all);
     dfree(p.d_gen);
@@ -141,7 +33,7 @@ static void free_plan(Plan& p) {
   p = Plan{};
 }
 
-static void refresh_state(bann_ctx* ctx) {
+void refresh_state(bann_ctx* ctx) {
   DevState& s = ctx->st;
   s.br = ctx->d_br;
   s.xu2 = ctx->d_xu2;
@@ -184,7 +76,7 @@ static void refresh_state(bann_ctx* ctx) {
   s.ows = ctx->d_ows;
 }
 
-static bool check_branch(const bann_ctx* ctx, int32_t b) {
+bool check_branch(const bann_ctx* ctx, int32_t b) {
   return ctx && ctx->finalized && b >= 0 && b < (int32_t)ctx->br.size();
 }
 
@@ -265,7 +157,7 @@ static void step_bases(const BranchHost& h, std::vector<double>& out) {
   }
 }
 
-static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent) {
+int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent) {
   free_plan(p);
   const int32_t nbr = (int32_t)ctx->br.size();
   if (nb > nbr) return fail(ctx, BANN_E_ARG, "branch list longer than the branch set");
@@ -357,7 +249,7 @@ static int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& 
 }
 
 // gradient (partials) of every branch in the plan at the current theta
-static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
+int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
@@ -374,13 +266,13 @@ static int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
 }
 
 // the fused leapfrog update of every branch in the plan (small and large kernels)
-static void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step) {
+void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step) {
   const int32_t nb = (int32_t)p.all.size();
   launch_update(ctx->st, p.d_all + nb, p.n_small, mode, step, ctx->stream, 0);
   launch_update(ctx->st, p.d_all + nb + p.n_small, p.n_large, mode, step, ctx->stream, 1);
 }
 
-static int ensure_htrace(bann_ctx* ctx, int32_t L) {
+int ensure_htrace(bann_ctx* ctx, int32_t L) {
   if (L + 1 <= ctx->htrace_cap) return BANN_OK;
   const int32_t cap = std::max({L + 1, 2 * ctx->htrace_cap, 129});  // grow geometrically: no realloc per trajectory
   dfree(ctx->d_htrace);
@@ -430,7 +322,9 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
                   ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
-                  ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows};
+                  ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
+                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart};
+  comm_destroy(ctx);
   for (void* p : bufs) dfree(p);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
@@ -1066,7 +960,7 @@ extern "C" int bann_neg_hamiltonian(bann_ctx* ctx, int32_t b, const float* momen
 // ---------------------------------------------------------------------------
 // HMC
 // ---------------------------------------------------------------------------
-static int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
+int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
                         const float* eps, const float* momentum, uint64_t seed, const float* u) {
   int rc = ensure_htrace(ctx, L);
   if (rc) return rc;

@@ -1,0 +1,240 @@
+// bann_dist.hip — multi-GPU entry points of include/bann.h: branch shards (one
+// process per GPU), the context's communicator (RCCL over xGMI, or a caller
+// all-reduce), the residual exchange of a leapfrog session, and the
+// network-joint HMC trajectory with its per-step all-reduce of the summed
+// branch outputs (north_star: "an RCCL all-reduce over xGMI only
+// for the summary-layer output and its gradient").
+//
+// The reference is single-device: Net::train (net.rs:251-334) visits the
+// branches one after another against a residual it refreshes in between.  The
+// branch-sharded equivalents here are (a) leapfrog sessions per rank with the
+// residual change exchanged per trajectory (the sweep bookkeeping of
+// net.rs:292-300 over ranks) and (b) one HMC state over all branches of all
+// ranks (network mode).
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "ctx_internal.h"
+
+void comm_destroy(bann_ctx* ctx) {
+  if (ctx->nccl) (void)ncclCommDestroy((ncclComm_t)ctx->nccl);
+  ctx->nccl = nullptr;
+  ctx->comm_kind = 0;
+}
+
+extern "C" int bann_shard_branches(const int32_t* marker_counts, int32_t nbranches, int32_t world,
+                                   int32_t* starts_out) {
+  if (!marker_counts || !starts_out || nbranches <= 0 || world <= 0 || world > nbranches) return BANN_E_ARG;
+  std::vector<int64_t> csum(nbranches + 1, 0);
+  for (int b = 0; b < nbranches; ++b) {
+    if (marker_counts[b] <= 0) return BANN_E_ARG;
+    csum[b + 1] = csum[b] + marker_counts[b];
+  }
+  starts_out[0] = 0;
+  for (int r = 1; r < world; ++r) {
+    // first branch whose prefix reaches r/world of the markers, leaving every
+    // rank at least one branch on either side
+    const double target = (double)csum[nbranches] * r / world;
+    int c = (int)(std::lower_bound(csum.begin(), csum.end(), (int64_t)ceil(target)) - csum.begin());
+    c = std::max(c, starts_out[r - 1] + 1);
+    c = std::min(c, nbranches - (world - r));
+    starts_out[r] = c;
+  }
+  starts_out[world] = nbranches;
+  return BANN_OK;
+}
+
+extern "C" int bann_comm_unique_id(uint8_t* id_out) {
+  if (!id_out) return BANN_E_ARG;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return BANN_E_HIP;
+  static_assert(sizeof(id) == 128, "RCCL unique id size");
+  memcpy(id_out, &id, sizeof(id));
+  return BANN_OK;
+}
+
+extern "C" int bann_ctx_comm_init(bann_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return BANN_E_ARG;
+  comm_destroy(ctx);
+  CK(hipSetDevice(ctx->device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t comm;
+  const ncclResult_t r = ncclCommInitRank(&comm, nranks, uid, rank);
+  if (r != ncclSuccess) return fail(ctx, BANN_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  ctx->nccl = comm;
+  ctx->comm_kind = 1;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return BANN_OK;
+}
+
+extern "C" int bann_ctx_comm_callback(bann_ctx* ctx, bann_allreduce_fn fn, void* user, int32_t nranks, int32_t rank) {
+  if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks) return BANN_E_ARG;
+  comm_destroy(ctx);
+  ctx->ar_fn = fn;
+  ctx->ar_user = user;
+  ctx->comm_kind = 2;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return BANN_OK;
+}
+
+extern "C" int bann_residual_update_host(bann_allreduce_fn fn, void* user, float* local_delta, float* residual,
+                                         int64_t n) {
+  if (!local_delta || !residual || n < 0) return BANN_E_ARG;
+  if (fn && fn(user, local_delta, n, 0) != 0) return BANN_E_HIP;
+  for (int64_t i = 0; i < n; ++i) residual[i] -= local_delta[i];  // net.rs:292-300
+  return BANN_OK;
+}
+
+// in-place sum over the ranks of n floats in a DEVICE buffer (on the context stream)
+static int allreduce_device_f32(bann_ctx* ctx, float* d, int64_t n) {
+  if (ctx->comm_kind == 1) {
+    const ncclResult_t r = ncclAllReduce(d, d, (size_t)n, ncclFloat32, ncclSum, (ncclComm_t)ctx->nccl, ctx->stream);
+    if (r != ncclSuccess) return fail(ctx, BANN_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  } else if (ctx->comm_kind == 2) {
+    std::vector<float> h(n);
+    CK(hipMemcpyAsync(h.data(), d, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    if (ctx->ar_fn(ctx->ar_user, h.data(), n, 0) != 0) return fail(ctx, BANN_E_HIP, "all-reduce callback failed");
+    CK(hipMemcpyAsync(d, h.data(), n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+  }
+  return BANN_OK;
+}
+
+// in-place sum over the ranks of n doubles in a HOST buffer
+static int allreduce_host_f64(bann_ctx* ctx, double* h, int64_t n) {
+  if (ctx->comm_kind == 1) {
+    double* d = nullptr;
+    CK(dalloc(&d, n));
+    CK(hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    const ncclResult_t r = ncclAllReduce(d, d, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)ctx->nccl, ctx->stream);
+    if (r != ncclSuccess) {
+      dfree(d);
+      return fail(ctx, BANN_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
+    CK(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    CK(hipStreamSynchronize(ctx->stream));
+    dfree(d);
+  } else if (ctx->comm_kind == 2) {
+    if (ctx->ar_fn(ctx->ar_user, h, n, 1) != 0) return fail(ctx, BANN_E_HIP, "all-reduce callback failed");
+  }
+  return BANN_OK;
+}
+
+extern "C" int bann_exchange_residual(bann_ctx* ctx, float* residual_host) {
+  if (!ctx || !residual_host) return BANN_E_ARG;
+  if (ctx->lf.all.empty() || ctx->lf_active) return fail(ctx, BANN_E_STATE, "call after bann_leapfrog_end");
+  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->d_delta_part, ctx->d_delta,
+                        ctx->stream);
+  CK(hipGetLastError());
+  if (ctx->comm_kind == 1) {  // sum over the ranks on the device (RCCL over xGMI), one copy back
+    int rc = allreduce_device_f32(ctx, ctx->d_delta, ctx->n);
+    if (rc) return rc;
+  }
+  CK(hipMemcpyAsync(ctx->h_delta, ctx->d_delta, ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  const bann_allreduce_fn fn = ctx->comm_kind == 2 ? ctx->ar_fn : nullptr;
+  const int rc = bann_residual_update_host(fn, ctx->ar_user, ctx->h_delta, residual_host, ctx->n);
+  return rc ? fail(ctx, rc, "residual exchange failed") : BANN_OK;
+}
+
+extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
+                                     float max_dh, int32_t step_mode, float factor, const float* eps,
+                                     const float* momentum, uint64_t seed, float u, int32_t* status_out,
+                                     double* h_trace_out, double* rss_out) {
+  if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (!y || L < 1) return fail(ctx, BANN_E_ARG, "null targets or L < 1");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  if (step_mode != BANN_STEP_IZMAILOV && step_mode != BANN_STEP_UNIFORM && step_mode != BANN_STEP_INJECTED)
+    return fail(ctx, BANN_E_ARG, "network mode: Izmailov, uniform or injected step sizes");
+  const int64_t n = ctx->n;
+  const int32_t nb = (int32_t)ctx->br.size();
+  if (!ctx->d_netsum) {
+    CK(dalloc(&ctx->d_netsum, n));
+    CK(dalloc(&ctx->d_nety, n));
+    CK(dalloc(&ctx->d_netpart, net_scratch_doubles(n)));
+  }
+  if (ctx->netrss_cap < L + 1) {
+    dfree(ctx->d_netrss);
+    ctx->d_netrss = nullptr;
+    CK(dalloc(&ctx->d_netrss, L + 1));
+    ctx->netrss_cap = L + 1;
+  }
+  std::vector<int32_t> all(nb);
+  for (int b = 0; b < nb; ++b) all[b] = b;
+  // every local branch, packed (the persistent plan of the leapfrog sessions is reused)
+  if (!(ctx->lf.owns && ctx->lf.all == all)) {
+    int rc = build_plan(ctx, all.data(), nb, ctx->lf, true);
+    if (rc) return rc;
+  }
+  const Plan& p = ctx->lf;
+  int rc = traj_prepare(ctx, p, L, max_dh, step_mode, factor, eps, momentum, seed, nullptr);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(ctx->d_nety, y, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  ctx->st.netmode = 1;
+  ctx->st.net_le = lambda_e;
+  // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
+  auto forward_and_targets = [&](int k) -> int {
+    int r = run_grad(ctx, p, 1);
+    if (r) return r;
+    launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->stream);
+    r = allreduce_device_f32(ctx, ctx->d_netsum, n);
+    if (r) return r;
+    launch_net_targets(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart, ctx->d_netrss + k,
+                       ctx->stream);
+    return run_grad(ctx, p, 0);
+  };
+  rc = forward_and_targets(0);
+  if (!rc) {
+    launch_snapshot_pred(ctx->st, p.d_all, nb, ctx->stream);
+    run_update(ctx, p, MODE_INIT, 0);
+    for (int k = 1; k <= L && !rc; ++k) {
+      rc = forward_and_targets(k);
+      if (!rc) run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
+    }
+  }
+  ctx->st.netmode = 0;
+  if (rc) return rc;
+  CK(hipGetLastError());
+  // network -H per step: sum over local branches (list order) and ranks, plus the rss term once
+  std::vector<double> tr((size_t)nb * ctx->htrace_cap), rss(L + 1), H(L + 1, 0.0);
+  CK(hipMemcpyAsync(tr.data(), ctx->d_htrace, tr.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(rss.data(), ctx->d_netrss, (L + 1) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k <= L; ++k)
+    for (int b = 0; b < nb; ++b) H[k] += tr[(size_t)b * ctx->htrace_cap + k];
+  rc = allreduce_host_f64(ctx, H.data(), L + 1);
+  if (rc) return rc;
+  for (int k = 0; k <= L; ++k) H[k] -= (double)lambda_e * rss[k] / 2.0;  // log_density_wrt_rss (100-102), once
+  int status = BANN_ACCEPTED;
+  for (int k = 1; k <= L; ++k)
+    if (fabs(H[k] - H[0]) > (double)max_dh) {  // early rejection (1264-1279)
+      status = BANN_REJECTED_EARLY;
+      break;
+    }
+  if (status == BANN_ACCEPTED) {  // one Metropolis decision for the network (928-962)
+    const double log_acc = H[L] - H[0];
+    const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
+    status = (double)u < acc_p ? BANN_ACCEPTED : BANN_REJECTED;
+  }
+  std::vector<int32_t> st(nb, status);
+  CK(hipMemcpyAsync(ctx->d_status, st.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  if (status != BANN_ACCEPTED) {  // every local branch back to theta_0, predictions to f(theta_0)
+    run_update(ctx, p, MODE_RESTORE, 0);
+    launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);
+  }
+  CK(hipGetLastError());
+  CK(hipStreamSynchronize(ctx->stream));
+  if (status_out) *status_out = status;
+  if (h_trace_out) std::copy(H.begin(), H.end(), h_trace_out);
+  if (rss_out) *rss_out = rss[L];
+  return BANN_OK;
+}

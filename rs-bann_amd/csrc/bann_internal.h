@@ -15,7 +15,7 @@
 #define BANN_FRAG 16         // individuals per fragment (MFMA N)
 #define BANN_TILE_FRAGS 4    // fragments per fused-kernel tile (64 individuals)
 
-enum { MODE_GRAD = 0, MODE_INIT = 1, MODE_STEP = 2, MODE_LAST = 3, MODE_PROFILE = 4 };
+enum { MODE_GRAD = 0, MODE_INIT = 1, MODE_STEP = 2, MODE_LAST = 3, MODE_PROFILE = 4, MODE_RESTORE = 5 };
 enum { ST_RUNNING = -1, ST_ACCEPTED = 0, ST_REJECTED = 1, ST_REJECTED_EARLY = 2 };
 
 // Per-branch descriptor (device resident, one per branch).
@@ -107,6 +107,8 @@ struct DevState {
   const int32_t* pidx;    // [sum P]: precision index (within the branch) of every parameter
   const float* ows;       // [nbranch][2]: output-weight summary stat of the OTHER branches (reg_sum), and
                           //   the network's output-weight count (OutputWeightSummaryStats, params.rs:404-465)
+  int32_t netmode;        // network-joint HMC: no per-branch rss term / decisions in k_update
+  float net_le;           // its error precision (every branch's)
   float hyper[6];         // NetworkPrecisionHyperparameters: (shape, scale) dense, summary, output (params.rs:134-142)
 };
 
@@ -133,6 +135,11 @@ void launch_update_joint(const DevState& st, const int32_t* branches, int32_t nb
 void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_q,
                                   uint64_t seed, hipStream_t s);
 #define BANN_JOINT_MAXQ 4608  // joint HMC: precisions per branch (ARD: m + hidden widths + L)
+void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s);
+// sum_e: in = sum over ranks of the branch outputs, out = the error e; part: net_scratch_doubles(n)
+void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
+                        float bias, double* part, double* rss_out, hipStream_t s);
+int64_t net_scratch_doubles(int64_t n);
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
 void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,

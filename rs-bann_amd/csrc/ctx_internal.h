@@ -1,0 +1,139 @@
+// ctx_internal.h — the bann_ctx context and the host helpers shared by the C-ABI
+// translation units (bann_api.hip: single-GPU API; bann_dist.hip: multi-GPU).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/bann.h"
+#include "bann_internal.h"
+
+struct BranchHost {
+  std::vector<int32_t> snp_idx;
+  std::vector<int32_t> widths;
+  int32_t m = 0, L = 0, act = 0, prior = 0;
+  int32_t P = 0, nprec = 0;
+  std::vector<float> prec;  // precision_vec order
+  float ows_reg_sum = 0.f;  // output-weight summary stat of the OTHER branches (joint HMC)
+  float ows_num = -1.f;     // output-weight count of the network (< 0: this branch's own)
+  BranchDev dev{};
+};
+
+// one packed gradient launch: every work item of one kernel instantiation
+struct LaunchGroup {
+  int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
+  int32_t L = 0, act = 0, nw = 1, full = 0;
+  std::vector<GradItem> items;
+  GradItem* d_items = nullptr;
+};
+
+struct Plan {
+  std::vector<int32_t> all, generic;
+  int32_t n_small = 0, n_large = 0;  // update kernels: d_all[nb .. nb+n_small) small, then n_large large
+  std::vector<LaunchGroup> groups;
+  int32_t max_p_generic = 0, max_p = 0;
+  int32_t* d_all = nullptr;
+  int32_t* d_gen = nullptr;
+  bool owns = false;
+};
+
+struct bann_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // genotypes
+  int64_t n = 0, M = 0;
+  int8_t* d_g = nullptr;
+  float* d_mu = nullptr;
+  float* d_sigma = nullptr;
+  // branches
+  std::vector<BranchHost> br;
+  bool finalized = false;
+  bool fused_enabled = true;
+  bool wide_bf16 = false;  // wx kernel: hidden GEMMs on bf16 MFMA (opt-in, reduced precision)
+  int32_t nfrag = 0, max_splits = 1;
+  int64_t packed_bytes = 0, total_p = 0;
+  // device buffers
+  BranchDev* d_br = nullptr;
+  uint8_t* d_xu2 = nullptr;  // 2-bit genotype tile images of every branch (u2t, kernels_fx.hip)
+  uint8_t* d_dig = nullptr;
+  FusedConst* d_fc = nullptr;
+  float *d_mub = nullptr, *d_sigb = nullptr;
+  float *d_theta = nullptr, *d_mom = nullptr, *d_eps = nullptr, *d_theta0 = nullptr, *d_lam = nullptr,
+        *d_lamld = nullptr, *d_grad = nullptr, *d_part = nullptr;
+  double* d_rss_part = nullptr;
+  float* d_pred0 = nullptr;
+  double* d_stepbase = nullptr;  // per-parameter Izmailov step base (sign: factor applies)
+  float *d_phi = nullptr, *d_phi0 = nullptr, *d_mphi = nullptr, *d_ephi = nullptr, *d_gphi = nullptr;  // joint HMC
+  int32_t* d_pidx = nullptr;
+  float* d_ows = nullptr;
+  int64_t total_q = 0;
+  float* d_delta = nullptr;       // n floats: residual change of the last trajectory (host-copy variant)
+  float* d_delta_part = nullptr;  // per-branch-slice partial rows of the residual change
+  int32_t* h_status = nullptr;    // pinned host mirrors (trajectory status, residual change)
+  float* h_delta = nullptr;
+  float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
+  double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
+  int32_t *d_status = nullptr, *d_uturn = nullptr;
+  int32_t htrace_cap = 0;  // L+1 capacity of d_htrace rows
+  // scratch plan buffers (per-call plans)
+  int32_t* d_list_scr = nullptr;
+  int32_t* d_gen_scr = nullptr;
+  GradItem* d_items_scr = nullptr;
+  unsigned long long* d_dbg = nullptr;  // BANN_STAMPS diagnostics
+  int64_t items_cap = 0;
+  // multi-GPU: one rank per GPU (bann_dist.hip)
+  int32_t comm_kind = 0;  // 0 none, 1 RCCL, 2 caller all-reduce callback
+  int32_t nranks = 1, rank = 0;
+  void* nccl = nullptr;   // ncclComm_t
+  bann_allreduce_fn ar_fn = nullptr;
+  void* ar_user = nullptr;
+  float* d_netsum = nullptr;   // network mode: n-vector sum of the local branch outputs, then the error e
+  float* d_nety = nullptr;     // network mode: the targets y
+  double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)
+  double* d_netpart = nullptr; // network mode: rss block partials
+  int32_t netrss_cap = 0;
+  // leapfrog session
+  Plan lf;
+  bool lf_active = false;
+  int32_t lf_L = 0, lf_step = 0;
+  DevState st{};
+};
+
+
+inline int fail(bann_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define CK(call)                                                                          \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(ctx, e_ == hipErrorOutOfMemory ? BANN_E_OOM : BANN_E_HIP,              \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                     \
+  } while (0)
+
+template <typename T>
+inline hipError_t dalloc(T** p, int64_t count) {
+  *p = nullptr;
+  if (count <= 0) count = 1;
+  return hipMalloc((void**)p, (size_t)count * sizeof(T));
+}
+
+inline void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+// implemented in bann_api.hip
+void refresh_state(bann_ctx* ctx);
+bool check_branch(const bann_ctx* ctx, int32_t b);
+int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent);
+void free_plan(Plan& p);
+int run_grad(bann_ctx* ctx, const Plan& p, int write_pred);
+void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step);
+int ensure_htrace(bann_ctx* ctx, int32_t L);
+int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
+                 const float* eps, const float* momentum, uint64_t seed, const float* u);

@@ -165,7 +165,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   }
   double rss = 0.0;
   for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
-  const float le = st.eprec[b];
+  const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
   const bool lasso = (bd.prior == 2 || bd.prior == 3);
   float th[UPD_CAP], gr[UPD_CAP], pm[UPD_CAP], ep[UPD_CAP], t0[UPD_CAP];
   double sums[3] = {0.0, 0.0, 0.0};
@@ -205,7 +205,8 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     return;
   }
   block_sum_n<NT, 3>(sums, redd);
-  const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
+  // + log_density_wrt_rss (100-102); network mode: the rss term is added once for the network by the host
+  const double ld = sums[0] - (st.netmode ? 0.0 : (double)le * rss / 2.0);
   const double h = ld - 0.5 * sums[1];                   // -H (878-883)
   const int stride = st.lint + 1;
   // what happens to theta: 0 = position step, 1 = restore theta0, 2 = keep
@@ -221,14 +222,20 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     }
   } else {
     const double h0 = st.h0[b];
-    const bool diverged = !prof && fabs(h - h0) > (double)st.max_dh;
+    const bool diverged = !prof && !st.netmode && fabs(h - h0) > (double)st.max_dh;
     if (!prof && t == 0) st.htrace[(int64_t)b * stride + step] = h;
     if (diverged) {  // RejectedEarly (1264-1279)
       act = 1;
       if (t == 0) st.status[b] = ST_REJECTED_EARLY;
     } else {
       if (!prof && t == 0 && sums[2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;  // 1281-1284
-      if (mode == MODE_LAST) {  // Metropolis (928-962)
+      if (mode == MODE_LAST && st.netmode) {  // network mode: the host decides for the network
+        act = 2;
+        if (t == 0) {
+          st.ld_out[b] = ld;
+          st.rss_out[b] = rss;
+        }
+      } else if (mode == MODE_LAST) {  // Metropolis (928-962)
         const double log_acc = h - h0;
         const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
         const bool accept = (double)st.uacc[b] < acc_p;
@@ -362,6 +369,14 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
   const int64_t base = bd.p_off;
   const bool prof = mode == MODE_PROFILE;
   if (prof) mode = MODE_STEP;
+  if (mode == MODE_RESTORE) {  // back to theta_0 (a rejected network trajectory)
+    for (int i = threadIdx.x; i < P; i += NT) st.theta[base + i] = st.theta0[base + i];
+    if (bd.fused) {
+      __syncthreads();
+      refresh_fused_const<NT>(st, b, bd);
+    }
+    return;
+  }
   if (!prof && (mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
   if ((bd.fused == 1 || bd.fused == 3) && P <= UPD_CAP * NT && bd.m <= MPT * NT && bd.widths[0] <= 4) {
     __shared__ float s_th[UPD_CAP * NT];
@@ -372,7 +387,7 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
   // ---- rss (fixed-order split reduction) ----
   double rss = 0.0;
   for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
-  const float le = st.eprec[b];
+  const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
   const bool lasso = (bd.prior == 2 || bd.prior == 3);
   // sums[0] = log prior (ridge_ard.rs:171-194 and the other priors), sums[1] =
   // sum p^2 (momentum.rs:149-158; INIT: the drawn momentum, else the
@@ -409,7 +424,8 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
     return;
   }
   block_sum_n<NT, 3>(sums, redd);
-  const double ld = sums[0] - (double)le * rss / 2.0;  // + log_density_wrt_rss (100-102)
+  // + log_density_wrt_rss (100-102); network mode: the rss term is added once for the network by the host
+  const double ld = sums[0] - (st.netmode ? 0.0 : (double)le * rss / 2.0);
   const double h = ld - 0.5 * sums[1];                   // -H = log density - K (878-883)
   const int stride = st.lint + 1;
   if (mode == MODE_INIT) {
@@ -431,7 +447,7 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
     }
   } else {
     const double h0 = st.h0[b];
-    const bool diverged = !prof && fabs(h - h0) > (double)st.max_dh;
+    const bool diverged = !prof && !st.netmode && fabs(h - h0) > (double)st.max_dh;
     if (!prof && threadIdx.x == 0) st.htrace[(int64_t)b * stride + step] = h;
     if (diverged) {  // RejectedEarly: restore the initial params (1264-1279)
       for (int i = threadIdx.x; i < P; i += NT) st.theta[base + i] = st.theta0[base + i];
@@ -450,6 +466,11 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
             st.mom[base + i] = p;
             st.theta[base + i] += e * p;
           }
+        }
+      } else if (st.netmode) {  // MODE_LAST, network mode: the host decides for the network
+        if (threadIdx.x == 0) {
+          st.ld_out[b] = ld;
+          st.rss_out[b] = rss;
         }
       } else {  // MODE_LAST: Metropolis decision (accept_or_reject_hmc_state, 928-962)
         const double log_acc = h - h0;
@@ -587,6 +608,74 @@ void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t 
   const unsigned gx = (unsigned)((st.n + 1023) / 1024);
   hipLaunchKernelGGL(k_residual_delta_part, dim3(gx, RD_GROUPS), dim3(256), 0, s, st, branches, nb, scratch);
   hipLaunchKernelGGL(k_residual_delta_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, scratch, st.n, out);
+}
+
+// network mode (bann_network_hmc_step): out[i] = sum over the listed branches of
+// pred[b][i], in list order (deterministic)
+__global__ void __launch_bounds__(256) k_net_sum(DevState st, const int32_t* __restrict__ blist, int nb,
+                                                 float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= st.n) return;
+  float s = 0.f;
+  for (int q = 0; q < nb; ++q) s += st.pred[(int64_t)blist[q] * st.n + i];
+  out[i] = s;
+}
+
+void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_net_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, st, branches, nb, out);
+}
+
+// e = sum f + bias - y (the network's output error, every branch's output
+// gradient), in place of the sum; each branch's target becomes y_b = f_b - e so
+// that the per-branch gradient kernels see e as their error; rss = sum e^2
+// (per-block partials, then a fixed-order sum: deterministic)
+#define NET_BLK 1024
+__global__ void __launch_bounds__(NET_BLK) k_net_err(int64_t n, float* __restrict__ sum_e, const float* __restrict__ y,
+                                                     float bias, double* __restrict__ part) {
+  __shared__ double red[NET_BLK / 64];
+  const int64_t i = (int64_t)blockIdx.x * NET_BLK + threadIdx.x;
+  double acc = 0.0;
+  if (i < n) {
+    const float e = sum_e[i] + bias - y[i];
+    sum_e[i] = e;
+    acc = (double)e * (double)e;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < NET_BLK / 64; ++w) t += red[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ void k_net_rss(const double* __restrict__ part, int nparts, double* __restrict__ rss_out) {
+  if (threadIdx.x != 0) return;
+  double t = 0.0;
+  for (int k = 0; k < nparts; ++k) t += part[k];
+  *rss_out = t;
+}
+
+__global__ void __launch_bounds__(256) k_net_targets(DevState st, const int32_t* __restrict__ blist,
+                                                     const float* __restrict__ e) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= st.n) return;
+  const int64_t o = (int64_t)blist[blockIdx.y] * st.n + i;
+  st.y[o] = st.pred[o] - e[i];
+}
+
+int64_t net_scratch_doubles(int64_t n) { return (n + NET_BLK - 1) / NET_BLK; }
+
+void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
+                        float bias, double* part, double* rss_out, hipStream_t s) {
+  const int nparts = (int)((st.n + NET_BLK - 1) / NET_BLK);
+  hipLaunchKernelGGL(k_net_err, dim3(nparts), dim3(NET_BLK), 0, s, st.n, sum_e, y, bias, part);
+  hipLaunchKernelGGL(k_net_rss, dim3(1), dim3(64), 0, s, part, nparts, rss_out);
+  if (nb > 0)
+    hipLaunchKernelGGL(k_net_targets, dim3((unsigned)((st.n + 255) / 256), (unsigned)nb), dim3(256), 0, s, st,
+                       branches, sum_e);
 }
 
 // pred <- pred0 for the listed branches that were not accepted (session end)

@@ -1,19 +1,21 @@
-"""Multi-rank path on CPU (gloo, world_size 2): branch sharding + the per-sweep
-residual all-reduce give the same network output / residual as one rank.
+"""Multi-rank path on CPU (gloo, world_size 2), driven through the library's C ABI:
+bann_shard_branches balances the branch ranges, and bann_residual_update_host --
+the exchange step bann_exchange_residual runs for a callback communicator --
+sums the ranks' residual changes through a gloo all-reduce callback
+(bann.distributed.TorchAllreduce); every rank ends with the single-rank residual.
 
-The per-branch compute here is the oracle (test infrastructure); what is under
-test is the sharding and exchange logic used by bench.py and the GPU driver."""
+The per-branch predictions come from the oracle (test infrastructure, there is
+no GPU here); what is under test is the library's sharding and exchange code."""
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import bann_oracle as O
-from bann.distributed import shard_ranges, update_residual
+from bann.distributed import TorchAllreduce, residual_update, shard_ranges
 
 
 def _free_port():
@@ -48,7 +50,7 @@ def _local_delta(rank, world):
         if accepted[b]:
             Xb = X[:, offs[b]:offs[b + 1]]
             d += O.predict(news[b], Xb) - O.predict(brs[b], Xb)
-    return d
+    return d.astype(np.float32)
 
 
 def _worker(rank, world, port, out):
@@ -56,10 +58,9 @@ def _worker(rank, world, port, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, ms, offs, X, brs, news, accepted, y = _problem()
-    residual = torch.tensor(y - sum(O.predict(brs[b], X[:, offs[b]:offs[b + 1]]) for b in range(len(ms))))
-    delta = torch.tensor(_local_delta(rank, world))
-    update_residual(residual, delta, dist)
-    out[rank] = residual.numpy().copy()
+    residual = (y - sum(O.predict(brs[b], X[:, offs[b]:offs[b + 1]]) for b in range(len(ms)))).astype(np.float32)
+    res = residual_update(residual, _local_delta(rank, world), TorchAllreduce(dist))
+    out[rank] = res.copy()
     dist.destroy_process_group()
 
 
@@ -69,6 +70,11 @@ def test_shard_ranges_balanced():
     assert all(b - a == 125 for a, b in r)
     r = shard_ranges([1, 1, 10, 1, 1, 10], 2)
     assert r[0][0] == 0 and r[-1][1] == 6 and r[0][1] == r[1][0]
+    # one dominant branch never leaves a rank empty
+    r = shard_ranges([1000, 1, 1, 1], 4)
+    assert r == [(0, 1), (1, 2), (2, 3), (3, 4)]
+    with pytest.raises(ValueError):   # more ranks than branches
+        shard_ranges([5, 5], 3)
 
 
 def test_sharded_residual_update_matches_single_rank():
@@ -78,7 +84,8 @@ def test_sharded_residual_update_matches_single_rank():
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
     n, ms, offs, X, brs, news, accepted, y = _problem()
-    ref = y - sum(O.predict(brs[b], X[:, offs[b]:offs[b + 1]]) for b in range(len(ms))) - _local_delta(0, 1)
+    ref = residual_update((y - sum(O.predict(brs[b], X[:, offs[b]:offs[b + 1]]) for b in range(len(ms)))
+                           ).astype(np.float32), _local_delta(0, 1), None)
     for r in range(world):
-        assert np.allclose(out[r], ref, rtol=0, atol=1e-10)
+        assert np.allclose(out[r], ref, rtol=0, atol=1e-5)
     assert np.array_equal(out[0], out[1])

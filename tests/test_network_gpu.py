@@ -1,0 +1,132 @@
+"""Network-joint HMC (bann_network_hmc_step): one HMC state over every branch,
+the per-step sum of branch outputs exchanged over the ranks.
+
+  * one rank: trajectory, -H trace, status and final parameters match the
+    oracle restatement (bann_oracle.network_hmc_step);
+  * two ranks on one GPU (two processes, two contexts, a gloo all-reduce
+    callback as the communicator -- RCCL needs one GPU per rank): the sharded
+    run reproduces the one-rank run (same status, -H trace within 1e-5, same
+    final parameters)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import bann_oracle as O
+from helpers import f32_branch, norm_rel, x_std
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(60, [4, 4, 1], "ridge_ard"), (40, [8, 8, 1], "lasso_base"), (700, [4, 4, 1], "ridge_base"),
+          (30, [6, 5, 3, 1], "lasso_ard")]
+
+
+def _problem(seed=5, n=800):
+    rng = np.random.default_rng(seed)
+    M = sum(m for m, _, _ in SHAPES)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w, prior in SHAPES:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior=prior))))
+        off += m
+    return rng, g, specs
+
+
+def _context(g, specs, branches):
+    from bann import BannContext
+    ctx = BannContext(0)
+    ctx.upload_genotypes(g)
+    for b in branches:
+        br = specs[b]["branch"]
+        ctx.add_branch(specs[b]["snps"], br.layer_widths, br.act, br.prior)
+    ctx.finalize()
+    for i, b in enumerate(branches):
+        br = specs[b]["branch"]
+        ctx.set_params(i, O.param_vec(br.weights, br.biases))
+        ctx.set_precisions(i, O.precision_vec(br))
+    return ctx
+
+
+def _draws(rng, specs, L):
+    eps, mom = [], []
+    for s in specs:
+        ew, eb = O.izmailov_step_sizes(s["branch"], 0.3, L)
+        eps.append(O.param_vec(ew, eb).astype(np.float32))
+        mom.append(rng.normal(size=s["branch"].num_params).astype(np.float32))
+    return eps, mom
+
+
+def test_network_hmc_matches_oracle():
+    rng, g, specs = _problem()
+    n, L = g.shape[1], 6
+    ctx = _context(g, specs, range(len(specs)))
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    f = sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+    y = (f + rng.normal(scale=0.7, size=n)).astype(np.float32).astype(np.float64)
+    bias, le = 0.25, 1.5
+    for u in (0.4, 0.999999):
+        eps, mom = _draws(rng, specs, L)
+        res = ctx.network_hmc_step(y, L, bias=bias, lambda_e=le, eps=np.concatenate(eps),
+                                   momentum=np.concatenate(mom), u=u)
+        brs = [s["branch"].copy() for s in specs]
+        out = O.network_hmc_step(brs, Xs, y, bias, le, [e.astype(np.float64) for e in eps],
+                                 [p.astype(np.float64) for p in mom], L, 10.0, u)
+        assert res["status"] == out["status"], (res["status"], out["status"])
+        tr = np.asarray(out["trace"])
+        assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (res["trace"], tr)
+        for b, br in enumerate(brs):
+            assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+        for s, br in zip(specs, brs):
+            s["branch"] = f32_branch(br)
+            s["branch"].error_precision = specs[0]["branch"].error_precision
+    ctx.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from bann.distributed import TorchAllreduce, shard_ranges
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng, g, specs = _problem(seed=9)
+    n, L = g.shape[1], 5
+    y = rng.normal(size=n).astype(np.float32)
+    eps, mom = _draws(rng, specs, L)
+    lo, hi = shard_ranges([m for m, _, _ in SHAPES], world)[rank]
+    ctx = _context(g, specs, range(lo, hi))
+    if world > 1:
+        ctx.comm_callback(TorchAllreduce(dist), world, rank)
+    res = ctx.network_hmc_step(y, L, bias=-0.1, lambda_e=0.8, eps=np.concatenate(eps[lo:hi]),
+                               momentum=np.concatenate(mom[lo:hi]), u=0.5)
+    out[rank] = dict(status=res["status"], trace=res["trace"],
+                     params=[ctx.get_params(i) for i in range(hi - lo)], lo=lo)
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_network_hmc_two_ranks_match_one():
+    import torch.multiprocessing as mp
+    results = {}
+    for world in (1, 2):
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.spawn(_rank_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        results[world] = dict(out)
+    one, two = results[1][0], results[2]
+    assert two[0]["status"] == two[1]["status"] == one["status"]
+    assert np.array_equal(two[0]["trace"], two[1]["trace"])   # identical network decision on every rank
+    assert np.all(np.abs(two[0]["trace"] - one["trace"]) <= 1e-5 * np.maximum(1.0, np.abs(one["trace"])))
+    params = two[0]["params"] + two[1]["params"]
+    for b, pv in enumerate(params):
+        assert norm_rel(pv, one["params"][b]) < 1e-5, b
