@@ -93,6 +93,27 @@ int bann_genotypes_set_stats(bann_ctx* ctx, const float* mu, const float* sigma)
 /* copy genotypes of markers snp_idx[0..m) back to the host as g[j*n + i] */
 int bann_genotypes_download(bann_ctx* ctx, const int32_t* snp_idx, int32_t m, int8_t* g_out);
 
+/* BedVM::from_file (bed.rs:193-245): stem.bed (3-byte signature checked;
+ * variant-major only, as the reference) with the dims of stem.dims or the line
+ * counts of stem.fam / stem.bim, streamed from the file into the device image
+ * in bounded blocks */
+int bann_genotypes_load_bed(bann_ctx* ctx, const char* stem);
+
+/* ---------------- files on either side of the path (host only, no device) ---------------- */
+/* BedDims (io/dims.rs:15-34): stem.dims "n M", else the .fam / .bim line counts */
+int bann_bed_dims(const char* stem, int64_t* n_out, int64_t* num_markers_out);
+/* ExternalGrouping::from_file (group/external.rs:15-60): two columns
+ * "marker_ix group_ix" (0-based, groups 0..G-1), as CSR: offsets[G+1],
+ * markers[num_entries] in file order.  Call with offsets/markers NULL for the sizes. */
+int bann_grouping_read(const char* path, int32_t* num_groups, int64_t* num_entries, int64_t* offsets,
+                       int32_t* markers);
+/* UniformGrouping::new (group/uniform.rs:11-23): group g = markers [g*size, (g+1)*size) */
+int bann_grouping_uniform(int32_t num_groups, int32_t group_size, int64_t* offsets, int32_t* markers);
+/* Phenotypes::from_file / to_file (data/phenotypes.rs:28-36): bincode Vec<f32>
+ * (u64 length + values, little endian).  bann_phen_read with y_out NULL gives n. */
+int bann_phen_read(const char* path, int64_t* n_out, float* y_out);
+int bann_phen_write(const char* path, const float* y, int64_t n);
+
 /* ---------------- branches: replaces BranchCfg -> B::from_cfg ----------------
  * branch_struct.rs:12-29 (from_cfg), branch_cfg.rs:185-193 (BranchCfg). */
 

@@ -85,6 +85,12 @@ SIGNATURES = {
     "bann_genotypes_upload_bed": (C.c_int, [_P, _pu8, _i64, _i64]),
     "bann_genotypes_synthetic": (C.c_int, [_P, _i64, _i64, _u64]),
     "bann_genotypes_stats": (C.c_int, [_P, _pf32, _pf32]),
+    "bann_genotypes_load_bed": (C.c_int, [_P, C.c_char_p]),
+    "bann_bed_dims": (C.c_int, [C.c_char_p, C.POINTER(_i64), C.POINTER(_i64)]),
+    "bann_grouping_read": (C.c_int, [C.c_char_p, _pi32, C.POINTER(_i64), C.POINTER(_i64), _pi32]),
+    "bann_grouping_uniform": (C.c_int, [_i32, _i32, C.POINTER(_i64), _pi32]),
+    "bann_phen_read": (C.c_int, [C.c_char_p, C.POINTER(_i64), _pf32]),
+    "bann_phen_write": (C.c_int, [C.c_char_p, _pf32, _i64]),
     "bann_genotypes_set_stats": (C.c_int, [_P, _pf32, _pf32]),
     "bann_genotypes_download": (C.c_int, [_P, _pi32, _i32, _pi8]),
     "bann_branch_add": (C.c_int, [_P, _pi32, _i32, _pi32, _i32, _i32, _i32]),

@@ -80,6 +80,12 @@ class BannContext:
         self._check(self._lib.bann_genotypes_upload_bed(self._h, _ptr(buf, C.c_uint8), n, num_markers))
         self.n, self.num_markers = n, num_markers
 
+    def load_bed(self, stem: str):
+        """PLINK stem.bed (+ .dims or .fam/.bim) streamed into the device image (bed.rs:193-245)."""
+        self._check(self._lib.bann_genotypes_load_bed(self._h, stem.encode()))
+        from .io import bed_dims
+        self.n, self.num_markers = bed_dims(stem)
+
     def synthetic_genotypes(self, n: int, num_markers: int, seed: int = 42):
         self._check(self._lib.bann_genotypes_synthetic(self._h, n, num_markers, seed))
         self.n, self.num_markers = n, num_markers

@@ -344,7 +344,7 @@ extern "C" int bann_synchronize(bann_ctx* ctx) {
 // ---------------------------------------------------------------------------
 // genotypes
 // ---------------------------------------------------------------------------
-static int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M) {
+int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M) {
   if (ctx->finalized) return fail(ctx, BANN_E_STATE, "genotypes must be set before bann_finalize");
   if (n <= 0 || M <= 0) return fail(ctx, BANN_E_SHAPE, "n and num_markers must be positive");
   CK(hipSetDevice(ctx->device));
@@ -355,20 +355,42 @@ static int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M) {
   ctx->d_mu = ctx->d_sigma = nullptr;
   ctx->n = n;
   ctx->M = M;
-  CK(dalloc(&ctx->d_g, n * M));
+  ctx->rowb = (n + 63) / 64 * 16;
+  CK(dalloc(&ctx->d_g, ctx->rowb * M));
   CK(dalloc(&ctx->d_mu, M));
   CK(dalloc(&ctx->d_sigma, M));
   return BANN_OK;
+}
+
+// markers per staged block: ~256 MiB of host input per copy
+int64_t stage_markers(int64_t bytes_per_marker, int64_t M) {
+  return std::max<int64_t>(1, std::min<int64_t>(M, (int64_t(256) << 20) / std::max<int64_t>(1, bytes_per_marker)));
 }
 
 extern "C" int bann_genotypes_upload(bann_ctx* ctx, const int8_t* g, int64_t n, int64_t num_markers) {
   if (!ctx || !g) return BANN_E_ARG;
   int rc = alloc_genotypes(ctx, n, num_markers);
   if (rc) return rc;
-  CK(hipMemcpyAsync(ctx->d_g, g, (size_t)(n * num_markers), hipMemcpyHostToDevice, ctx->stream));
-  launch_col_stats(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
-  CK(hipGetLastError());
+  // int8 [M][n] streamed through a bounded staging block, packed to 2 bits on the device
+  const int64_t blk = stage_markers(n, num_markers);
+  int8_t* d_st = nullptr;
+  int32_t* d_flag = nullptr;
+  int32_t flag = 0;
+  CK(dalloc(&d_st, blk * n));
+  CK(dalloc(&d_flag, 1));
+  CK(hipMemsetAsync(d_flag, 0, sizeof(int32_t), ctx->stream));
+  for (int64_t j0 = 0; j0 < num_markers; j0 += blk) {
+    const int64_t m = std::min(blk, num_markers - j0);
+    CK(hipMemcpyAsync(d_st, g + j0 * n, (size_t)(m * n), hipMemcpyHostToDevice, ctx->stream));
+    launch_i8_to_raw(d_st, n, m, ctx->d_g + j0 * ctx->rowb, ctx->rowb, d_flag, ctx->stream);
+    CK(hipGetLastError());
+  }
+  launch_col_stats(ctx->d_g, ctx->rowb, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
+  CK(hipMemcpyAsync(&flag, d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
+  dfree(d_st);
+  dfree(d_flag);
+  if (flag) return fail(ctx, BANN_E_ARG, "genotypes must be 2-bit codes in 0..3 (.bed semantics)");
   return BANN_OK;
 }
 
@@ -376,15 +398,21 @@ extern "C" int bann_genotypes_upload_bed(bann_ctx* ctx, const uint8_t* payload, 
   if (!ctx || !payload) return BANN_E_ARG;
   int rc = alloc_genotypes(ctx, n, num_markers);
   if (rc) return rc;
-  const int64_t bytes = ((n + 3) / 4) * num_markers;
-  uint8_t* d_pl = nullptr;
-  CK(dalloc(&d_pl, bytes));
-  CK(hipMemcpyAsync(d_pl, payload, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
-  launch_decode_bed(d_pl, ctx->d_g, n, num_markers, ctx->stream);
-  launch_col_stats(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
+  // payload rows streamed through a bounded staging block, decoded into the 2-bit image
+  const int64_t bpc = (n + 3) / 4;
+  const int64_t blk = stage_markers(bpc, num_markers);
+  uint8_t* d_st = nullptr;
+  CK(dalloc(&d_st, blk * bpc));
+  for (int64_t j0 = 0; j0 < num_markers; j0 += blk) {
+    const int64_t m = std::min(blk, num_markers - j0);
+    CK(hipMemcpyAsync(d_st, payload + j0 * bpc, (size_t)(m * bpc), hipMemcpyHostToDevice, ctx->stream));
+    launch_bed_to_raw(d_st, n, m, ctx->d_g + j0 * ctx->rowb, ctx->rowb, ctx->stream);
+    CK(hipGetLastError());
+  }
+  launch_col_stats(ctx->d_g, ctx->rowb, ctx->d_mu, ctx->d_sigma, n, num_markers, ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
-  dfree(d_pl);
+  dfree(d_st);
   return BANN_OK;
 }
 
@@ -392,7 +420,7 @@ extern "C" int bann_genotypes_synthetic(bann_ctx* ctx, int64_t n, int64_t num_ma
   if (!ctx) return BANN_E_ARG;
   int rc = alloc_genotypes(ctx, n, num_markers);
   if (rc) return rc;
-  launch_synthetic_genotypes(ctx->d_g, ctx->d_mu, ctx->d_sigma, n, num_markers, seed, ctx->stream);
+  launch_synthetic_genotypes(ctx->d_g, ctx->rowb, ctx->d_mu, ctx->d_sigma, n, num_markers, seed, ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
   return BANN_OK;
@@ -424,7 +452,7 @@ extern "C" int bann_genotypes_download(bann_ctx* ctx, const int32_t* snp_idx, in
   CK(dalloc(&d_idx, m));
   CK(dalloc(&d_out, (int64_t)m * ctx->n));
   CK(hipMemcpyAsync(d_idx, snp_idx, m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-  launch_unpack_markers(ctx->d_g, d_idx, m, ctx->n, d_out, ctx->stream);
+  launch_unpack_markers(ctx->d_g, ctx->rowb, d_idx, m, ctx->n, d_out, ctx->stream);
   CK(hipMemcpyAsync(g_out, d_out, (size_t)m * ctx->n, hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   dfree(d_idx);
@@ -551,19 +579,6 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
              h.widths[1] <= BANN_WIDE_MAXW)
       d.fused = 2;
     if (d.fused) total_frags += ctx->nfrag;
-  }
-  // every kernel reads 2-bit genotype codes (.bed semantics: 0, 1, 2; 3 is accepted)
-  {
-    int32_t* d_flag = nullptr;
-    int32_t flag = 0;
-    CK(dalloc(&d_flag, 1));
-    CK(hipMemsetAsync(d_flag, 0, sizeof(int32_t), ctx->stream));
-    launch_check_2bit(ctx->d_g, n * ctx->M, d_flag, ctx->stream);
-    CK(hipGetLastError());
-    CK(hipMemcpyAsync(&flag, d_flag, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));
-    dfree(d_flag);
-    if (flag) return fail(ctx, BANN_E_ARG, "genotypes must be 2-bit codes in 0..3 (.bed semantics)");
   }
   int64_t target_items = 1024;  // wx (and fx with BANN_TARGET_ITEMS / BANN_MIN_FRAGS): ~target work items
   if (const char* e = getenv("BANN_TARGET_ITEMS")) target_items = std::max<int64_t>(1, atoll(e));
@@ -726,37 +741,47 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_gen_scr, nb));
   CK(dalloc(&ctx->d_items_scr, items));
   ctx->items_cap = items;
-  // pack genotypes and gather marker statistics per branch
+  // every branch's tile image in ONE batched pack launch (no per-branch sync), the
+  // marker statistics in one gather, the precision-derived arrays in one copy each
+  std::vector<int32_t> allidx;
+  allidx.reserve(mk_off);
+  std::vector<PackJob> jobs;
+  for (auto& h : ctx->br) {
+    const int32_t base = (int32_t)allidx.size();
+    allidx.insert(allidx.end(), h.snp_idx.begin(), h.snp_idx.end());
+    for (int c = 0; c < h.dev.nchunks; ++c)
+      jobs.push_back(PackJob{h.dev.x_off + 1024ll * c, 1024ll * h.dev.nchunks, base + 64 * c,
+                             std::min(64, h.m - 64 * c)});
+  }
   int32_t* d_idx = nullptr;
-  int32_t maxm = 0;
-  for (auto& h : ctx->br) maxm = std::max(maxm, h.m);
-  CK(dalloc(&d_idx, maxm));
+  PackJob* d_jobs = nullptr;
+  CK(dalloc(&d_idx, (int64_t)allidx.size()));
+  CK(dalloc(&d_jobs, (int64_t)jobs.size()));
+  CK(hipMemcpyAsync(d_idx, allidx.data(), allidx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(d_jobs, jobs.data(), jobs.size() * sizeof(PackJob), hipMemcpyHostToDevice, ctx->stream));
+  launch_pack_tiles(ctx->d_g, ctx->rowb, d_jobs, (int32_t)jobs.size(), d_idx, ntile, ctx->d_xu2, ctx->stream);
+  launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, (int32_t)allidx.size(), ctx->d_mub, ctx->d_sigb, ctx->stream);
+  CK(hipGetLastError());
   std::vector<BranchDev> descs;
-  std::vector<float> lam, lamld, eprec(nb, 1.f);
-  std::vector<double> sbase;
+  std::vector<float> lam_all(p_off), lamld_all(p_off), eprec(nb, 1.f), lam, lamld;
+  std::vector<double> sbase_all(p_off), sbase;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
-    CK(hipMemcpyAsync(d_idx, h.snp_idx.data(), h.m * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    launch_pack_branch_u2t(ctx->d_g, d_idx, h.m, n, ctx->d_xu2 + h.dev.x_off, h.dev.nchunks, (int32_t)ntile,
-                           ctx->stream);
-    launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, h.m, ctx->d_mub + h.dev.mk_off, ctx->d_sigb + h.dev.mk_off,
-                        ctx->stream);
-    CK(hipGetLastError());
-    CK(hipStreamSynchronize(ctx->stream));  // d_idx reused
     descs.push_back(h.dev);
     float ep = 1.f;
     expand_precisions(h, lam, lamld, ep);
     eprec[b] = ep;
-    CK(hipMemcpyAsync(ctx->d_lam + h.dev.p_off, lam.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
-                      ctx->stream));
-    CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
-                      ctx->stream));
     step_bases(h, sbase);
-    CK(hipMemcpyAsync(ctx->d_stepbase + h.dev.p_off, sbase.data(), h.P * sizeof(double), hipMemcpyHostToDevice,
-                      ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));  // host vectors reused
+    std::copy(lam.begin(), lam.end(), lam_all.begin() + h.dev.p_off);
+    std::copy(lamld.begin(), lamld.end(), lamld_all.begin() + h.dev.p_off);
+    std::copy(sbase.begin(), sbase.end(), sbase_all.begin() + h.dev.p_off);
   }
+  CK(hipMemcpyAsync(ctx->d_lam, lam_all.data(), p_off * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_lamld, lamld_all.data(), p_off * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_stepbase, sbase_all.data(), p_off * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
   dfree(d_idx);
+  dfree(d_jobs);
   CK(dalloc(&ctx->d_br, nb));
   CK(hipMemcpyAsync(ctx->d_br, descs.data(), nb * sizeof(BranchDev), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_eprec, eprec.data(), nb * sizeof(float), hipMemcpyHostToDevice, ctx->stream));

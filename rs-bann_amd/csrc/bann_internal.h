@@ -113,12 +113,25 @@ struct DevState {
 };
 
 // ---- launchers (defined in the kernel translation units) ----
-void launch_synthetic_genotypes(int8_t* g, float* mu, float* sigma, int64_t n, int64_t M, uint64_t seed,
-                                hipStream_t s);
-void launch_decode_bed(const uint8_t* payload, int8_t* g, int64_t n, int64_t M, hipStream_t s);
-void launch_col_stats(const int8_t* g, float* mu, float* sigma, int64_t n, int64_t M, hipStream_t s);
-void launch_unpack_markers(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, int8_t* out,
-                           hipStream_t s);
+// one chunk (64 marker rows) of one branch's tile image: batched pack (kernels_data.hip)
+struct PackJob {
+  int64_t dst;          // byte offset of the chunk in tile 0 of the branch's image (x_off + 1024 c)
+  int64_t tile_stride;  // bytes per tile of the branch's image (1024 nchunks)
+  int32_t idx_off;      // first of the chunk's rows in the concatenated marker-index list
+  int32_t rows;         // valid rows (markers) of the chunk, <= 64; the rest are zero padding
+};
+// genotype image: 2-bit variant-major rows of rowb = ceil(n/64)*16 bytes (kernels_data.hip header)
+void launch_synthetic_genotypes(uint8_t* raw, int64_t rowb, float* mu, float* sigma, int64_t n, int64_t M,
+                                uint64_t seed, hipStream_t s);
+void launch_i8_to_raw(const int8_t* g, int64_t n, int64_t m, uint8_t* raw, int64_t rowb, int32_t* flag,
+                      hipStream_t s);
+void launch_bed_to_raw(const uint8_t* payload, int64_t n, int64_t m, uint8_t* raw, int64_t rowb, hipStream_t s);
+void launch_col_stats(const uint8_t* raw, int64_t rowb, float* mu, float* sigma, int64_t n, int64_t M,
+                      hipStream_t s);
+void launch_unpack_markers(const uint8_t* raw, int64_t rowb, const int32_t* snp_idx, int32_t m, int64_t n,
+                           int8_t* out, hipStream_t s);
+void launch_pack_tiles(const uint8_t* raw, int64_t rowb, const PackJob* jobs, int32_t njobs, const int32_t* idx,
+                       int64_t ntile, uint8_t* dst, hipStream_t s);
 void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp_idx, int32_t m, float* mu_b,
                          float* sig_b, hipStream_t s);
 
@@ -141,7 +154,6 @@ void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb,
                         float bias, double* part, double* rss_out, hipStream_t s);
 int64_t net_scratch_doubles(int64_t n);
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
-void launch_check_2bit(const int8_t* g, int64_t count, int32_t* flag, hipStream_t s);  // flag |= any g not in 0..3
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
                           int write_pred, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
@@ -149,8 +161,6 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                            int32_t nw, int full, int write_pred, hipStream_t s);
 int fxl_lds_bytes(int nw, int nl);
-void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
-                            int32_t nchunks, int32_t ntile, hipStream_t s);
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
                        int izmailov, float c, int32_t L, hipStream_t s);
 void launch_restore_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);

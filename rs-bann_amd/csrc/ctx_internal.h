@@ -45,7 +45,8 @@ struct bann_ctx {
   std::string err;
   // genotypes
   int64_t n = 0, M = 0;
-  int8_t* d_g = nullptr;
+  uint8_t* d_g = nullptr;  // 2-bit variant-major genotype image (kernels_data.hip), rowb bytes per marker
+  int64_t rowb = 0;
   float* d_mu = nullptr;
   float* d_sigma = nullptr;
   // branches
@@ -135,5 +136,7 @@ void free_plan(Plan& p);
 int run_grad(bann_ctx* ctx, const Plan& p, int write_pred);
 void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step);
 int ensure_htrace(bann_ctx* ctx, int32_t L);
+int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M);   // the 2-bit genotype image of n x M
+int64_t stage_markers(int64_t bytes_per_marker, int64_t M);  // markers per ~256 MiB staging block
 int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
                  const float* eps, const float* momentum, uint64_t seed, const float* u);

@@ -1141,41 +1141,3 @@ void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t ni
     default: break;
   }
 }
-
-// ---- "u2t" tile-row genotype image (see the header comment) ----
-__global__ void k_pack_u2t(const int8_t* __restrict__ g, const int32_t* __restrict__ idx, int32_t m, int64_t n,
-                           uint8_t* __restrict__ dst, int32_t nchunks, int32_t ntile) {
-  const int rows = 64 * nchunks;
-  const int64_t total = (int64_t)ntile * rows;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(t % rows);
-    const int64_t tile = t / rows;
-    uint8_t q[16];
-#pragma unroll
-    for (int Q = 0; Q < 16; ++Q) {
-      uint32_t v = 0;
-      if (j < m) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int64_t row = 64 * tile + 4 * Q + p;
-          if (row < n) v |= ((uint32_t)g[(int64_t)idx[j] * n + row] & 3u) << (2 * p);
-        }
-      }
-      q[Q] = (uint8_t)v;
-    }
-    const int w = j >> 4, P = ((j & 15) + 8 * (w & 1)) & 15, sw = P >> 3;
-    uint8_t* o = dst + tile * (int64_t)rows * 16 + (16 * w + P) * 16;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int bq = 0; bq < 8; ++bq) o[8 * (h ^ sw) + bq] = q[8 * h + bq];
-  }
-}
-
-void launch_pack_branch_u2t(const int8_t* g, const int32_t* snp_idx, int32_t m, int64_t n, uint8_t* dst,
-                            int32_t nchunks, int32_t ntile, hipStream_t s) {
-  const int64_t total = (int64_t)ntile * 64 * nchunks;
-  const int64_t blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(k_pack_u2t, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, s, g, snp_idx, m, n,
-                     dst, nchunks, ntile);
-}

@@ -675,3 +675,54 @@ def test_hmc_step_joint_refuses_std_normal_and_reports_shapes(Ctx):
     with pytest.raises(ValueError):   # eps must cover parameters AND precisions
         ctx.hmc_step_joint([0], 3, HYPER, eps=np.ones(br.num_params, np.float32))
     ctx.close()
+
+
+# ------------------------------------------------------------ ingestion (f3)
+PLINK = os.path.join(HERE, "golden", "plink")
+
+
+def test_load_bed_file_small_and_random(Ctx):
+    """bann_genotypes_load_bed streams stem.bed into the 2-bit device image: the
+    reference's small fileset (dims from .fam/.bim) decodes to the matrix of
+    resources/test/README.md with the reference's column statistics; random.bed
+    (dims from random.dims) decodes like the oracle's bed_decode of its bytes."""
+    bs = KAT["bed_small"]
+    ctx = Ctx(0)
+    ctx.load_bed(os.path.join(PLINK, "small"))
+    g = ctx.download_genotypes(np.arange(bs["m"]))
+    assert np.array_equal(g.reshape(-1).astype(np.float32), np.array(bs["data_f32_col_major"], np.float32))
+    mu, sd = ctx.genotype_stats()
+    assert np.allclose(mu, bs["col_means"], rtol=0, atol=1e-6)
+    assert np.allclose(sd, bs["col_stds"], rtol=1e-6, atol=1e-7)
+    ctx.close()
+    raw = open(os.path.join(PLINK, "random.bed"), "rb").read()
+    ctx = Ctx(0)
+    ctx.load_bed(os.path.join(PLINK, "random"))
+    g = ctx.download_genotypes(np.arange(20))
+    assert np.array_equal(g, O.bed_decode(raw[3:], 100, 20))
+    ctx.close()
+
+
+def test_upload_paths_agree_and_reject_non_2bit(Ctx):
+    """int8 upload (streamed, packed on the device), .bed payload upload and
+    download agree bit for bit; an int8 value outside 0..3 is refused."""
+    rng = np.random.default_rng(12)
+    n, M = 1003, 77
+    g = O.synthetic_genotypes(rng, n, M)
+    a = Ctx(0)
+    a.upload_genotypes(g)
+    b = Ctx(0)
+    b.upload_bed(O.bed_encode(g), n, M)
+    assert np.array_equal(a.download_genotypes(np.arange(M)), g)
+    assert np.array_equal(b.download_genotypes(np.arange(M)), g)
+    for x, y in zip(a.genotype_stats(), b.genotype_stats()):
+        assert np.array_equal(x, y)
+    a.close()
+    b.close()
+    from bann import BannError
+    bad = g.copy()
+    bad[3, 5] = 4
+    c = Ctx(0)
+    with pytest.raises(BannError):
+        c.upload_genotypes(bad)
+    c.close()
