@@ -192,6 +192,17 @@ int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L,
                   const float* u, int32_t* status_out, double* h_trace_out, int32_t* uturn_out,
                   double* log_density_out);
 
+/* trajectory recording (MCMCCfg::trajectories, trajectory.rs:1-43,
+ * branch_sampler.rs:1253-1289): while enabled, bann_hmc_step keeps per listed
+ * branch the parameters after every position step, the log-density gradient
+ * there and the -H trace (host copies after every launch: a debugging aid) */
+int bann_set_trajectory_recording(bann_ctx* ctx, int32_t enabled);
+/* the last recorded trajectory of branch b: steps taken (an early rejection
+ * stops it), params[steps][P] and ldg[steps][P] in param_vec order,
+ * hamiltonian[steps + 1]; at most cap steps are copied; outputs may be NULL */
+int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap, int32_t* steps, float* params, float* ldg,
+                               double* hamiltonian);
+
 /* ---------------- joint HMC: replaces hmc_step_joint (branch_sampler.rs:1070-1178) ----------------
  * One trajectory per listed branch over its parameters AND its precisions
  * (ridge / lasso priors; std_normal has no joint density and is refused),

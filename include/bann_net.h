@@ -55,6 +55,8 @@ typedef struct {
   int32_t burn_in;
   int32_t fixed_param_precisions;
   int32_t sampled_output_bias;
+  int32_t trace;         /* outdir/trace: the BranchCfgs as a JSON line after init and every sweep (net.rs:241-244, 350-353) */
+  int32_t trajectories;  /* outdir/traj: one JSON Trajectory line per HMC step (trajectory.rs, branch_sampler.rs:1196-1289) */
 } bann_mcmc_cfg;
 
 /* Host random source for the driver's draws (the reference's ThreadRng,
@@ -100,6 +102,13 @@ int bann_net_set_rng_hooks(bann_net* net, const bann_rng_hooks* hooks);
 /* override GlobalParams / OutputBias (e.g. to continue a loaded chain) */
 int bann_net_set_global(bann_net* net, float error_precision, float output_layer_precision, float output_bias,
                         float output_bias_precision);
+/* test data of record_perf (net.rs:597-610: mse_test = rss / n_test): a
+ * context over the test cohort with the same branches (count, markers, layer
+ * widths) and targets y_test[n_test]; the driver copies its current
+ * parameters there at every record.  NULL detaches (mse_test: None). */
+int bann_net_set_test_data(bann_net* net, bann_ctx* test_ctx, const float* y_test, int64_t n_test);
+/* the recorded mse_test series (min(cap, records) entries); 0 entries without test data */
+int bann_net_records_test(const bann_net* net, float* mse_test, int32_t cap);
 /* Net::train (net.rs:201-358) on the phenotype y[n].  outdir (may be NULL):
  * models/<chain_ix>.bin after burn-in (net.rs:338-342, 565-569) and
  * training_stats (JSON, train_stats.rs:83-87). */

@@ -52,7 +52,7 @@ class McmcCfg(C.Structure):
     _fields_ = [("hmc_step_size_factor", C.c_float), ("hmc_max_hamiltonian_error", C.c_float),
                 ("hmc_integration_length", C.c_int32), ("hmc_step_size_mode", C.c_int32),
                 ("chain_length", C.c_int32), ("burn_in", C.c_int32), ("fixed_param_precisions", C.c_int32),
-                ("sampled_output_bias", C.c_int32)]
+                ("sampled_output_bias", C.c_int32), ("trace", C.c_int32), ("trajectories", C.c_int32)]
 
 
 # bann_allreduce_fn: in-place sum over ranks of a host buffer (dtype 0 f32, 1 f64)
@@ -147,6 +147,10 @@ SIGNATURES = {
     "bann_net_summary": (C.c_int, [_P, C.POINTER(TrainSummary)]),
     "bann_net_records": (C.c_int, [_P, _pf32, _pf32, _i32]),
     "bann_net_residual": (C.c_int, [_P, _pf32]),
+    "bann_net_set_test_data": (C.c_int, [_P, _P, _pf32, _i64]),
+    "bann_net_records_test": (C.c_int, [_P, _pf32, _i32]),
+    "bann_set_trajectory_recording": (C.c_int, [_P, _i32]),
+    "bann_branch_get_trajectory": (C.c_int, [_P, _i32, _i32, _pi32, _pf32, _pf32, _pf64]),
     "bann_net_save": (C.c_int, [_P, C.c_char_p]),
     "bann_net_load": (C.c_int, [_P, C.c_char_p]),
     "bann_net_last_error": (C.c_char_p, [_P]),

@@ -255,6 +255,21 @@ class BannContext:
             _ptr(status, C.c_int32), _ptr(trace, C.c_double), _ptr(uturn, C.c_int32), _ptr(ld, C.c_double)))
         return dict(status=status, trace=trace, uturn=uturn, log_density=ld)
 
+    def set_trajectory_recording(self, enabled: bool):
+        self._check(self._lib.bann_set_trajectory_recording(self._h, 1 if enabled else 0))
+
+    def get_trajectory(self, b: int):
+        """last recorded trajectory of branch b: dict(params [steps, P], ldg [steps, P], hamiltonian [steps+1])."""
+        steps = C.c_int32()
+        self._check(self._lib.bann_branch_get_trajectory(self._h, b, 0, C.byref(steps), None, None, None))
+        k, P = steps.value, self.num_params(b)
+        pr = np.zeros((k, P), np.float32)
+        lg = np.zeros((k, P), np.float32)
+        h = np.zeros(k + 1, np.float64)
+        self._check(self._lib.bann_branch_get_trajectory(self._h, b, k, C.byref(steps), _ptr(pr, C.c_float),
+                                                         _ptr(lg, C.c_float), _ptr(h, C.c_double)))
+        return dict(params=pr, ldg=lg, hamiltonian=h)
+
     def set_output_stats(self, b: int, reg_sum_others: float, num_params: float):
         """OutputWeightSummaryStats of branch b for the joint density (params.rs:404-465)."""
         self._check(self._lib.bann_branch_set_output_stats(self._h, b, float(reg_sum_others), float(num_params)))

@@ -34,12 +34,15 @@ class MCMCConfig:
     burn_in: Optional[int] = None
     fixed_param_precisions: bool = False
     sampled_output_bias: bool = False
+    trace: bool = False          # outdir/trace: BranchCfgs as JSON per sweep (net.rs:241-244, 350-353)
+    trajectories: bool = False   # outdir/traj: one Trajectory JSON per HMC step (trajectory.rs)
 
     def to_c(self) -> McmcCfg:
         burn = self.chain_length - 1 if self.burn_in is None else self.burn_in
         return McmcCfg(self.hmc_step_size_factor, self.hmc_max_hamiltonian_error, self.hmc_integration_length,
                        STEP_MODES[self.hmc_step_size_mode], self.chain_length, max(burn, 0),
-                       int(self.fixed_param_precisions), int(self.sampled_output_bias))
+                       int(self.fixed_param_precisions), int(self.sampled_output_bias), int(self.trace),
+                       int(self.trajectories))
 
 
 class Net:
@@ -106,6 +109,24 @@ class Net:
         self._check(self._lib.bann_net_records(self._h, mse.ctypes.data_as(C.POINTER(C.c_float)),
                                                lpd.ctypes.data_as(C.POINTER(C.c_float)), k))
         return mse, lpd
+
+    def set_test_data(self, test_ctx, y_test):
+        """record_perf's test set (net.rs:597-610): a context over the test cohort with the
+        same branches; None detaches."""
+        if test_ctx is None:
+            self._check(self._lib.bann_net_set_test_data(self._h, None, None, 0))
+            self._test = None
+            return
+        y = np.ascontiguousarray(y_test, dtype=np.float32)
+        self._test = (test_ctx, y)   # the context must outlive the net's use of it
+        self._check(self._lib.bann_net_set_test_data(self._h, test_ctx._h, y.ctypes.data_as(C.POINTER(C.c_float)),
+                                                     y.size))
+
+    def records_test(self) -> np.ndarray:
+        k = self._lib.bann_net_records_test(self._h, None, 0)
+        out = np.zeros(max(k, 0), np.float32)
+        self._check(self._lib.bann_net_records_test(self._h, out.ctypes.data_as(C.POINTER(C.c_float)), out.size))
+        return out
 
     def residual(self) -> np.ndarray:
         out = np.zeros(self._ctx.n, np.float32)

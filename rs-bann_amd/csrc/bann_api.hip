@@ -1074,14 +1074,45 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
     return BANN_OK;
   }
   run_update(ctx, p, MODE_INIT, 0);
+  if (ctx->rec_on) {  // params[k-1] = theta_k (after the k-th position step), ldg[k-1] = its gradient
+    ctx->rec.resize(ctx->br.size());
+    for (int i = 0; i < nb; ++i) {
+      auto& R = ctx->rec[branches[i]];
+      R.params.assign((size_t)L * ctx->br[branches[i]].P, 0.f);
+      R.ldg.assign((size_t)L * ctx->br[branches[i]].P, 0.f);
+    }
+  }
   for (int k = 1; k <= L; ++k) {
     rc = run_grad(ctx, p, k == L ? 1 : 0);
     if (rc) return rc;
+    if (ctx->rec_on)
+      for (int i = 0; i < nb; ++i) {
+        const BranchHost& h = ctx->br[branches[i]];
+        CK(hipMemcpyAsync(ctx->rec[branches[i]].params.data() + (size_t)(k - 1) * h.P, ctx->d_theta + h.dev.p_off,
+                          h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+      }
     run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
+    if (ctx->rec_on)
+      for (int i = 0; i < nb; ++i) {
+        const BranchHost& h = ctx->br[branches[i]];
+        CK(hipMemcpyAsync(ctx->rec[branches[i]].ldg.data() + (size_t)(k - 1) * h.P, ctx->d_grad + h.dev.p_off,
+                          h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+      }
   }
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
   const int stride = ctx->htrace_cap;
+  if (ctx->rec_on)
+    for (int i = 0; i < nb; ++i) {  // -H trace; an early rejection leaves the later entries unwritten (NaN)
+      auto& R = ctx->rec[branches[i]];
+      R.h.assign(L + 1, 0.0);
+      CK(hipMemcpy(R.h.data(), ctx->d_htrace + (int64_t)branches[i] * stride, (L + 1) * sizeof(double),
+                   hipMemcpyDeviceToHost));
+      int steps = 0;
+      while (steps < L && R.h[steps + 1] == R.h[steps + 1]) ++steps;
+      R.steps = steps;
+      R.h.resize(steps + 1);
+    }
   for (int i = 0; i < nb; ++i) {
     const int b = branches[i];
     if (status_out) CK(hipMemcpy(status_out + i, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -1182,6 +1213,26 @@ extern "C" int bann_hmc_step_joint(bann_ctx* ctx, const int32_t* branches, int32
     rc = upload_precisions(ctx, b);
     if (rc) return rc;
   }
+  return BANN_OK;
+}
+
+extern "C" int bann_set_trajectory_recording(bann_ctx* ctx, int32_t enabled) {
+  if (!ctx) return BANN_E_ARG;
+  ctx->rec_on = enabled != 0;
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap, int32_t* steps, float* params,
+                                          float* ldg, double* hamiltonian) {
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  if (b >= (int32_t)ctx->rec.size() || ctx->rec[b].h.empty()) return fail(ctx, BANN_E_STATE, "no recorded trajectory");
+  const auto& R = ctx->rec[b];
+  const int64_t P = ctx->br[b].P;
+  const int32_t k = std::min(cap, R.steps);
+  if (steps) *steps = R.steps;
+  if (params) std::copy(R.params.begin(), R.params.begin() + k * P, params);
+  if (ldg) std::copy(R.ldg.begin(), R.ldg.begin() + k * P, ldg);
+  if (hamiltonian) std::copy(R.h.begin(), R.h.begin() + k + 1, hamiltonian);
   return BANN_OK;
 }
 

@@ -144,6 +144,9 @@ struct bann_net {
   // LogPosteriorDensity (log_posterior_density.rs:9-16)
   float lpd_rss = -INFINITY, lpd_outw = -INFINITY;
   std::vector<float> lpd_local;
+  // test data of record_perf (net.rs:597-610)
+  bann_ctx* test_ctx = nullptr;
+  std::vector<float> y_test, mse_test;
 };
 
 namespace {
@@ -307,12 +310,133 @@ void update_lpd(bann_net* t, int b, double others) {
                        le * (rss / 2.0 + 1.0 / t->hp.output_scale));
 }
 
-// Net::record_perf (net.rs:597-610), without test data
-void record_perf(bann_net* t) {
+// Net::record_perf (net.rs:597-610); with test data: Net::mse (644-646) = rss / n
+// of the network prediction sum_b f_b + bias on the test cohort
+int record_perf(bann_net* t) {
   double l = (double)t->lpd_rss + t->lpd_outw;
   for (float v : t->lpd_local) l += v;
   t->lpd.push_back((float)l);
   t->mse.push_back((float)(sum_sq(t->residual.data(), t->n) / (double)t->n));
+  if (t->test_ctx) {
+    const int nb = (int)t->br.size();
+    const int64_t nt = (int64_t)t->y_test.size();
+    std::vector<int32_t> all(nb);
+    for (int b = 0; b < nb; ++b) {
+      all[b] = b;
+      const int rc = bann_branch_set_params(t->test_ctx, b, t->br[b].params.data());
+      if (rc < 0) return fail(t, rc, std::string("test context: ") + bann_last_error(t->test_ctx));
+    }
+    std::vector<float> preds((size_t)nb * nt);
+    const int rc = bann_predict_many(t->test_ctx, all.data(), nb, preds.data());
+    if (rc < 0) return fail(t, rc, std::string("test context: ") + bann_last_error(t->test_ctx));
+    double rss = 0.0;
+    for (int64_t i = 0; i < nt; ++i) {
+      double f = t->ob_bias;
+      for (int b = 0; b < nb; ++b) f += preds[(size_t)b * nt + i];
+      const double r = (double)t->y_test[i] - f;
+      rss += r * r;
+    }
+    t->mse_test.push_back((float)(rss / (double)nt));
+  }
+  return BANN_OK;
+}
+
+// serde_json of a float (non-finite values have no JSON form: serde writes null)
+void jf(std::string& o, double v) {
+  char buf[32];
+  if (std::isfinite(v))
+    std::snprintf(buf, sizeof(buf), "%.9g", v);
+  else
+    std::snprintf(buf, sizeof(buf), "null");
+  o += buf;
+}
+void jvec(std::string& o, const float* p, int64_t k) {
+  o += '[';
+  for (int64_t i = 0; i < k; ++i) {
+    if (i) o += ',';
+    jf(o, p[i]);
+  }
+  o += ']';
+}
+void jvec_u(std::string& o, const std::vector<int>& v) {
+  o += '[';
+  for (size_t i = 0; i < v.size(); ++i) o += (i ? "," : "") + std::to_string(v[i]);
+  o += ']';
+}
+
+// the branch_cfgs as serde_json (BranchCfg, branch_cfg.rs:7-16 and params.rs:192-199, 468-476)
+std::string trace_line(const bann_net* t) {
+  static const char* acts[] = {"Tanh", "ReLU", "LeakyReLU", "SiLU", "Identity"};
+  std::string o = "[";
+  for (size_t bi = 0; bi < t->br.size(); ++bi) {
+    const Branch& B = t->br[bi];
+    if (bi) o += ',';
+    o += "{\"num_params\":" + std::to_string(B.P) + ",\"num_weights\":" + std::to_string(B.num_weights) +
+         ",\"num_markers\":" + std::to_string(B.m) + ",\"layer_widths\":";
+    jvec_u(o, B.widths);
+    o += ",\"params\":{\"weights\":[";
+    for (int l = 0; l < B.L; ++l) {
+      if (l) o += ',';
+      jvec(o, B.params.data() + B.woff[l], (int64_t)B.win[l] * B.widths[l]);
+    }
+    o += "],\"biases\":[";
+    for (int l = 0; l < B.L - 1; ++l) {
+      if (l) o += ',';
+      jvec(o, B.params.data() + B.boff[l], B.widths[l]);
+    }
+    o += "],\"layer_widths\":";
+    jvec_u(o, B.widths);
+    o += ",\"num_markers\":" + std::to_string(B.m) + ",\"output_weight_summary_stats\":{\"reg_sum\":";
+    jf(o, B.ows_reg_sum);
+    o += ",\"num_params\":" + std::to_string(B.ows_num) + "}},\"precisions\":{\"weight_precisions\":[";
+    for (int l = 0; l < B.L; ++l) {
+      if (l) o += ',';
+      jvec(o, B.prec.data() + B.wpoff[l], B.wpn[l]);
+    }
+    o += "],\"bias_precisions\":[";
+    for (int l = 0; l < B.L - 1; ++l) {
+      if (l) o += ',';
+      jvec(o, B.prec.data() + B.bpoff + l, 1);
+    }
+    o += "],\"error_precision\":";
+    jvec(o, B.prec.data() + B.epoff, 1);
+    o += "},\"activation_function\":\"" + std::string(acts[B.act]) + "\"}";
+  }
+  return o + "]\n";
+}
+
+// one Trajectory (trajectory.rs:3-11) of the last hmc_step of branch b as serde_json
+int traj_line(bann_net* t, int b, std::string& o) {
+  const Branch& B = t->br[b];
+  int32_t steps = 0;
+  CKB(bann_branch_get_trajectory(t->ctx, b, 0, &steps, nullptr, nullptr, nullptr));
+  std::vector<float> pr((size_t)steps * B.P), lg((size_t)steps * B.P);
+  std::vector<double> h(steps + 1);
+  CKB(bann_branch_get_trajectory(t->ctx, b, steps, &steps, pr.data(), lg.data(), h.data()));
+  o = "{\"params\":[";
+  for (int k = 0; k < steps; ++k) {
+    if (k) o += ',';
+    jvec(o, pr.data() + (size_t)k * B.P, B.P);
+  }
+  o += "],\"precisions\":[],\"ldg\":[";
+  for (int k = 0; k < steps; ++k) {
+    if (k) o += ',';
+    jvec(o, lg.data() + (size_t)k * B.P, B.P);
+  }
+  o += "],\"num_ldg\":[],\"hamiltonian\":[";
+  for (int k = 0; k <= steps; ++k) {
+    if (k) o += ',';
+    jf(o, (float)h[k]);
+  }
+  o += "]}\n";
+  return BANN_OK;
+}
+
+int append_text(bann_net* t, const std::string& path, const std::string& text) {
+  FILE* f = std::fopen(path.c_str(), "a");
+  if (!f) return fail(t, BANN_E_ARG, "cannot open " + path);
+  const bool ok = std::fwrite(text.data(), 1, text.size(), f) == text.size();
+  return (std::fclose(f) == 0 && ok) ? BANN_OK : fail(t, BANN_E_ARG, "short write to " + path);
 }
 
 bool mkdir_p(const std::string& d) {
@@ -367,7 +491,12 @@ Writer serialize(const bann_net* t) {
   w.u64(t->nacc);
   w.u64(t->nearly);
   w.vf32(t->mse.data(), t->mse.size());
-  w.u8(0);  // mse_test: None
+  if (t->test_ctx) {  // mse_test: Option<Vec<f32>>
+    w.u8(1);
+    w.vf32(t->mse_test.data(), t->mse_test.size());
+  } else {
+    w.u8(0);
+  }
   w.vf32(t->lpd.data(), t->lpd.size());
   w.f32(t->lpd_rss);  // LogPosteriorDensity
   w.f32(t->lpd_outw);
@@ -396,7 +525,13 @@ int write_training_stats(bann_net* t, const std::string& dir) {  // train_stats.
   std::fprintf(f, "{\"num_samples\":%llu,\"num_accepted\":%llu,\"num_early_rejected\":%llu,\"mse_train\":[",
                (unsigned long long)t->ns, (unsigned long long)t->nacc, (unsigned long long)t->nearly);
   for (size_t i = 0; i < t->mse.size(); ++i) std::fprintf(f, i ? ",%.9g" : "%.9g", t->mse[i]);
-  std::fprintf(f, "],\"mse_test\":null,\"lpd\":[");
+  if (t->test_ctx) {
+    std::fprintf(f, "],\"mse_test\":[");
+    for (size_t i = 0; i < t->mse_test.size(); ++i) std::fprintf(f, i ? ",%.9g" : "%.9g", t->mse_test[i]);
+    std::fprintf(f, "],\"lpd\":[");
+  } else {
+    std::fprintf(f, "],\"mse_test\":null,\"lpd\":[");
+  }
   for (size_t i = 0; i < t->lpd.size(); ++i) std::fprintf(f, i ? ",%.9g" : "%.9g", t->lpd[i]);
   std::fprintf(f, "]}");
   std::fclose(f);
@@ -527,7 +662,17 @@ extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann
     for (int64_t i = 0; i < n; ++i) t->residual[i] -= pred[i];
     update_lpd(t, b, others);
   }
-  record_perf(t);
+  {
+    const int rc = record_perf(t);
+    if (rc) return rc;
+  }
+  const bool trace = cfg->trace && !dir.empty(), traj = cfg->trajectories && !dir.empty();
+  if (trace) {  // File::create (net.rs:213-215): a fresh trace, the initial cfgs first (241-244)
+    std::remove((dir + "/trace").c_str());
+    const int rc = append_text(t, dir + "/trace", trace_line(t));
+    if (rc) return rc;
+  }
+  CKB(bann_set_trajectory_recording(t->ctx, traj ? 1 : 0));
   if (!dir.empty() && cfg->burn_in == 0) {
     const int rc = write_file(t, dir + "/models/0.bin");
     if (rc) return rc;
@@ -565,6 +710,12 @@ extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann
       CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error,
                         cfg->hmc_step_size_mode, cfg->hmc_step_size_factor, nullptr, mom.data(), 0, &u, &status,
                         nullptr, nullptr, nullptr));
+      if (traj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
+        std::string line;
+        int rc = traj_line(t, b, line);
+        if (!rc) rc = append_text(t, dir + "/traj", line);
+        if (rc) return rc;
+      }
       ++t->ns;  // TrainingStats::add_hmc_step_result (train_stats.rs:46-53)
       if (status == BANN_ACCEPTED) ++t->nacc;
       if (status == BANN_REJECTED_EARLY) ++t->nearly;
@@ -598,14 +749,49 @@ extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann
       }
       for (int64_t i = 0; i < n; ++i) t->residual[i] -= t->ob_bias;
     }
-    record_perf(t);
+    {
+      const int rc = record_perf(t);
+      if (rc) return rc;
+    }
+    if (trace) {
+      const int rc = append_text(t, dir + "/trace", trace_line(t));
+      if (rc) return rc;
+    }
     if (!dir.empty() && chain_ix >= cfg->burn_in) {
       const int rc = write_file(t, dir + "/models/" + std::to_string(chain_ix) + ".bin");
       if (rc) return rc;
     }
   }
+  CKB(bann_set_trajectory_recording(t->ctx, 0));
   if (!dir.empty()) return write_training_stats(t, dir);
   return BANN_OK;
+}
+
+extern "C" int bann_net_set_test_data(bann_net* t, bann_ctx* test_ctx, const float* y_test, int64_t n_test) {
+  if (!t) return BANN_E_ARG;
+  if (!test_ctx) {
+    t->test_ctx = nullptr;
+    t->y_test.clear();
+    return BANN_OK;
+  }
+  if (!y_test || n_test <= 0) return fail(t, BANN_E_ARG, "null or empty test targets");
+  if (bann_num_branches(test_ctx) != (int)t->br.size()) return fail(t, BANN_E_SHAPE, "test context branch count");
+  for (int b = 0; b < (int)t->br.size(); ++b) {
+    int32_t m = 0, L = 0, w[8] = {0};
+    if (bann_branch_info(test_ctx, b, &m, &L, w, 8, nullptr, nullptr) != BANN_OK || m != t->br[b].m ||
+        L != t->br[b].L || !std::equal(w, w + L, t->br[b].widths.begin()))
+      return fail(t, BANN_E_SHAPE, "test context branches differ from the training branches");
+  }
+  t->test_ctx = test_ctx;
+  t->y_test.assign(y_test, y_test + n_test);
+  return BANN_OK;
+}
+
+extern "C" int bann_net_records_test(const bann_net* t, float* mse_test, int32_t cap) {
+  if (!t) return BANN_E_ARG;
+  const int32_t k = std::min<int32_t>(cap, (int32_t)t->mse_test.size());
+  if (mse_test) std::copy(t->mse_test.begin(), t->mse_test.begin() + k, mse_test);
+  return (int)t->mse_test.size();
 }
 
 extern "C" int bann_net_summary(const bann_net* t, bann_train_summary* out) {

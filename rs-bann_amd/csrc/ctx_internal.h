@@ -96,6 +96,14 @@ struct bann_ctx {
   double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)
   double* d_netpart = nullptr; // network mode: rss block partials
   int32_t netrss_cap = 0;
+  // trajectory recording (mcmc_cfg.trajectories, trajectory.rs): per branch of the last bann_hmc_step
+  bool rec_on = false;
+  struct Rec {
+    int32_t steps = 0;
+    std::vector<float> params, ldg;  // [L][P]
+    std::vector<double> h;           // [L + 1]
+  };
+  std::vector<Rec> rec;  // indexed by branch
   // leapfrog session
   Plan lf;
   bool lf_active = false;

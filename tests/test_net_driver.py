@@ -169,3 +169,101 @@ def test_training_reduces_mse():
     assert np.all(np.isfinite(lpd))
     net.close()
     ctx.close()
+
+
+def test_trace_trajectories_and_test_mse(tmp_path):
+    """f2: MCMCCfg::trace writes the BranchCfgs as one serde-JSON line after init
+    and after every sweep (net.rs:241-244, 350-353); MCMCCfg::trajectories one
+    Trajectory JSON per HMC step (trajectory.rs:3-11, branch_sampler.rs:1253-1289);
+    a test set gives record_perf's mse_test (net.rs:597-610) in training_stats
+    and in the model file."""
+    from bann import BannContext, MCMCConfig, Net
+    ctx, branches, X, y = build("ridge_ard", seed=5)
+    rng = np.random.default_rng(77)
+    ms = (40, 64, 30)
+    gt = O.synthetic_genotypes(rng, 300, sum(ms))
+    tctx = BannContext(0)
+    tctx.upload_genotypes(gt)
+    off = 0
+    for m, br in zip(ms, branches):
+        tctx.add_branch(np.arange(off, off + m, dtype=np.int32), br.layer_widths, "tanh", "ridge_ard")
+        off += m
+    tctx.finalize()
+    y_test = rng.normal(size=300).astype(np.float32)
+    net = Net(ctx, seed=3)
+    net.set_test_data(tctx, y_test)
+    L, chain = 4, 3
+    net.train(y, MCMCConfig(hmc_integration_length=L, chain_length=chain, trace=True, trajectories=True),
+              outdir=str(tmp_path))
+    lines = open(tmp_path / "trace").read().splitlines()
+    assert len(lines) == chain + 1
+    last = json.loads(lines[-1])
+    assert len(last) == 3 and last[0]["activation_function"] == "Tanh"
+    for b, cfg in enumerate(last):
+        w = [np.asarray(v, np.float32) for v in cfg["params"]["weights"]]
+        bb = [np.asarray(v, np.float32) for v in cfg["params"]["biases"]]
+        assert np.array_equal(np.concatenate(w + bb), ctx.get_params(b))
+        assert cfg["num_params"] == ctx.num_params(b) and cfg["layer_widths"] == list(branches[b].layer_widths)
+    trajs = [json.loads(t) for t in open(tmp_path / "traj").read().splitlines()]
+    assert len(trajs) == chain * 3
+    for t in trajs:
+        k = len(t["params"])
+        assert 1 <= k <= L and len(t["ldg"]) == k and len(t["hamiltonian"]) == k + 1
+        assert t["precisions"] == [] and t["num_ldg"] == []
+    mt = net.records_test()
+    mse, _ = net.records()
+    assert mt.size == mse.size == chain + 1
+    mu, sd = tctx.genotype_stats()
+    off, f = 0, np.zeros(300)
+    for b, m in enumerate(ms):
+        s = np.arange(off, off + m)
+        off += m
+        bw, bb = O.load_param_vec(ctx.get_params(b).astype(np.float64), m, branches[b].layer_widths)
+        br = branches[b].copy()
+        br.weights, br.biases = bw, bb
+        f += O.predict(br, x_std(gt[s], mu[s], sd[s]))
+    f += net.summary()["output_bias"]
+    assert rel(float(mt[-1]), float(np.mean((y_test - f) ** 2))) < 1e-4
+    js = json.load(open(tmp_path / "training_stats"))
+    assert np.allclose(js["mse_test"], mt, rtol=1e-6)
+    fm = NO.read_net_file(str(tmp_path / "models" / f"{chain}.bin"))
+    assert np.array_equal(np.float32(fm["training_stats"]["mse_test"]), mt)
+    for o in (net, ctx, tctx):
+        o.close()
+
+
+def test_trajectory_recording_matches_oracle_hmc():
+    """bann_set_trajectory_recording: the recorded parameters, gradients and -H of
+    an injected-draw trajectory are the oracle's (params after each position
+    step, ldg at them, the -H trace)."""
+    from bann import BannContext
+    ctx, branches, X, y = build("lasso_ard", seed=8)
+    br = branches[0]
+    ctx.set_target(0, y)
+    L = 5
+    ew, eb = O.izmailov_step_sizes(br, 0.5, L)
+    eps = O.param_vec(ew, eb).astype(np.float32)
+    p0 = np.random.default_rng(1).normal(size=br.num_params).astype(np.float32)
+    ctx.set_trajectory_recording(True)
+    res = ctx.hmc_step([0], L, 10.0, eps=eps, momentum=p0, u=[0.5])
+    tr = ctx.get_trajectory(0)
+    assert tr["params"].shape == (L, br.num_params) and tr["hamiltonian"].size == L + 1
+    assert np.array_equal(tr["hamiltonian"], res["trace"][0])
+    ob = br.copy()
+    pw, pb = O.load_param_vec(p0.astype(np.float64), br.num_markers, br.layer_widths)
+    ew2, eb2 = O.load_param_vec(eps.astype(np.float64), br.num_markers, br.layer_widths)
+    th = O.param_vec(ob.weights, ob.biases)
+    gw, gb, _ = O.log_density_gradient(ob, X[0], y.astype(np.float64))
+    p = O.param_vec(pw, pb)
+    e = O.param_vec(ew2, eb2)
+    g = O.param_vec(gw, gb)
+    for k in range(L):   # the oracle leapfrog, recording like branch_sampler.rs:1239-1262
+        p = p + 0.5 * e * g
+        th = th + e * p
+        ob.weights, ob.biases = O.load_param_vec(th, br.num_markers, br.layer_widths)
+        gw, gb, _ = O.log_density_gradient(ob, X[0], y.astype(np.float64))
+        g = O.param_vec(gw, gb)
+        p = p + 0.5 * e * g
+        assert norm_rel(tr["params"][k], th) < 1e-5, k
+        assert norm_rel(tr["ldg"][k], g) < 1e-5, k
+    ctx.close()
