@@ -40,6 +40,9 @@ CONFIGS = {
     # C5 (BASELINE.json configs[4]): 4k branches of 125 SNPs (500k-SNP panel),
     # 100k individuals, W = S = 32: the wide kernel, hidden GEMMs on MFMA
     "c5": (100_000, 500_000, 4000, [32, 32, 1]),
+    # C3's cohort with the reference's DEFAULT architecture: hidden and summary
+    # widths m_b / 2 (cli.rs:365-375) -- the layered gx path (f32 MFMA GEMMs)
+    "c3def": (50_000, 500_000, 1000, [250, 250, 1]),
 }
 METRIC = "HMC leapfrog steps/sec (whole node), 50k indiv × 500k SNP × 1k branches"
 HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md)
@@ -93,10 +96,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--step-factor", type=float, default=None,
-                    help="Izmailov factor c; default 1.0 (cli.rs:99-100), 0.15 for c5 (acceptance ~0.7 at L = 100)")
+                    help="Izmailov factor c; default 1.0 (cli.rs:99-100), 0.15 for c5, 0.02 for c3def (wide branches: acceptance > 0.6)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-branches", type=int, default=96)   # capped at the config's branch count
-    ap.add_argument("--cpu-sample-steps", type=int, default=16)
+    ap.add_argument("--cpu-sample-branches", type=int, default=None)   # default 96 (c3def: 4), capped at the branch count
+    ap.add_argument("--cpu-sample-steps", type=int, default=None)      # default 16 (c3def: 2)
     ap.add_argument("--profile-iters", type=int, default=10)
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="profiling only: run rank 0's shard of an N-GPU job on this one GPU, no collective")
@@ -129,7 +132,12 @@ def main():
     if args.step_factor is None:
         # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
         # curvature, c = 1 rejects every trajectory; c = 0.15 accepts ~0.7
-        args.step_factor = 0.15 if args.config == "c5" else 1.0
+        args.step_factor = {"c5": 0.15, "c3def": 0.02}.get(args.config, 1.0)
+    heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
+    if args.cpu_sample_branches is None:
+        args.cpu_sample_branches = 4 if heavy else 96
+    if args.cpu_sample_steps is None:
+        args.cpu_sample_steps = 2 if heavy else 16
     m_b = M_total // B_total
     b0, b1 = shard_ranges([m_b] * B_total, max(world, args.emulate_shard))[rank]   # contiguous, balanced by markers
     nb = b1 - b0
@@ -141,8 +149,10 @@ def main():
     for k in range(nb):
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
-    wide = widths[0] > 4
-    assert all(ctx.kernel_path(k) == ("wide" if wide else ("fused" if m_b <= 512 else "fused_large")) for k in range(nb))
+    path = ctx.kernel_path(0)
+    assert path == ("layered" if heavy else "wide" if widths[0] > 4 else "fused" if m_b <= 512 else "fused_large")
+    assert all(ctx.kernel_path(k) == path for k in range(nb))
+    wide = path in ("wide", "layered")   # MFMA-bound: hidden-layer GEMMs
     if args.hidden_bf16:
         ctx.set_hidden_gemm_bf16(True)
     params, precs, out_ss = [], [], 0.0
@@ -243,7 +253,8 @@ def main():
     workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
                 "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else "") +
                 (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else ""))
-    kernel_name = "k_fused_grad_wx" if wide else ("k_fused_grad_fx" if m_b <= 512 else "k_fused_grad_fxl")
+    kernel_name = {"wide": "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
+                   "layered": "k_gx_gemm"}[path]
     # ---- kernel timing for the roofline (HIP events on the library stream) ----
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
     grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
@@ -263,6 +274,8 @@ def main():
     # forward Z1 = A0 W1, error propagation err0 = delta1 W1^T and dW1 = A0^T delta1,
     # 2 n W S flops each per branch (branch_sampler.rs:760-771, 844-866)
     hidden_flops = 3 * 2 * n * widths[0] * widths[1] * nb
+    if path == "layered":   # gx: every GEMM on the f32 MFMA -- masked layer forward + dW0, hidden GEMMs
+        hidden_flops += 2 * 2 * n * m_b * widths[0] * nb
     # the masked layer on the i8 MFMA: W0 and delta0 as 4 digits, forward + backward
     i8_ops = 2 * 2 * n * m_b * 4 * widths[0] * nb
     # HBM traffic per gradient launch, from the committed PMC pass of the same
@@ -309,7 +322,9 @@ def main():
                           "peak": BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                           "frac": hidden_flops / (grad_ms * 1e-3) / 1e12 /
                           (BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF),
-                          "basis": "hidden-layer GEMM flops 6 n W S per branch per launch",
+                          "basis": ("f32 MFMA GEMM flops 4 n m W + 6 n W S per branch per launch (the whole "
+                                    "gradient evaluation: FWD0, FWD1, BWD1, GRAD1, GRAD0)") if path == "layered" else
+                                   "hidden-layer GEMM flops 6 n W S per branch per launch",
                           "i8_mfma_tops": i8_ops / (grad_ms * 1e-3) / 1e12,
                           "mfma_busy_pmc": (mfma_pmc or {}).get("mfma_busy_per_simd_cycle"),
                           "hbm_GBps": achieved} if wide else

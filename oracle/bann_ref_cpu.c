@@ -112,7 +112,8 @@ static double leapfrog_step(Branch* B, float* p, float* g, const float* eps, con
   for (int i = 0; i < P; ++i) g[i] = 0.f;
 #pragma omp parallel
   {
-    float l_dW1[64 * 64], l_dwo[64], l_db0[64], l_db1[64];
+    float* l_dW1 = (float*)malloc(sizeof(float) * ((size_t)W * S + 2 * S + 2 * W));
+    float *l_dwo = l_dW1 + W * S, *l_db0 = l_dwo + S, *l_db1 = l_db0 + W, *err0 = l_db1 + S;
     memset(l_dW1, 0, sizeof(float) * W * S);
     memset(l_dwo, 0, sizeof(float) * S);
     memset(l_db0, 0, sizeof(float) * W);
@@ -120,7 +121,6 @@ static double leapfrog_step(Branch* B, float* p, float* g, const float* eps, con
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
       const float e = out[i] - B->y[i];
-      float err0[64];
       for (int j = 0; j < W; ++j) err0[j] = 0.f;
       for (int k = 0; k < S; ++k) {
         const float a1 = A1[(int64_t)k * n + i];
@@ -146,6 +146,7 @@ static double leapfrog_step(Branch* B, float* p, float* g, const float* eps, con
       for (int q = 0; q < W; ++q) db0[q] += l_db0[q];
       for (int q = 0; q < S; ++q) db1[q] += l_db1[q];
     }
+    free(l_dW1);
   }
   /* dW0 = (delta0^T X)^T : second pass over X */
 #pragma omp parallel for schedule(static)
@@ -178,7 +179,6 @@ static double leapfrog_step(Branch* B, float* p, float* g, const float* eps, con
  */
 double bann_ref_cpu_bench(int64_t n, int m, int W, int S, int nbranch, int nsteps, uint64_t seed, int threads,
                           double* setup_s, double* checksum) {
-  if (W > 64 || S > 64) return -1.0;
   if (threads > 0) omp_set_num_threads(threads);
   const int P = m * W + W * S + S + W + S;
   Branch B;

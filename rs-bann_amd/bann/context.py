@@ -135,9 +135,9 @@ class BannContext:
 
     def kernel_path(self, b: int) -> str:
         """"fused" (fx: widths <= 4, m <= 512), "fused_large" (fxl: widths <= 4, m <= 4096),
-        "wide" (wx: one hidden layer <= 32 x 32, m <= 128) or "generic"."""
+        "wide" (wx: one hidden layer <= 32 x 32, m <= 128) or "layered" (gx: any shape, layered MFMA GEMMs)."""
         return {1: "fused", 2: "wide", 3: "fused_large"}.get(
-            self._check(self._lib.bann_branch_kernel_path(self._h, b)), "generic")
+            self._check(self._lib.bann_branch_kernel_path(self._h, b)), "layered")
 
     def set_hidden_gemm_bf16(self, enabled: bool):
         """wide kernel: hidden GEMMs on bf16 MFMA (reduced precision) instead of f32 MFMA."""

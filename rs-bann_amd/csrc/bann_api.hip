@@ -27,7 +27,8 @@ void comm_destroy(bann_ctx* ctx);  // bann_dist.hip
 void free_plan(Plan& p) {
   if (p.owns) {
     dfree(p.d_all);
-    dfree(p.d_gen);
+    dfree(p.d_gx);
+    dfree(p.d_gxpre);
     for (auto& g : p.groups) dfree(g.d_items);
   }
   p = Plan{};
@@ -183,8 +184,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     const BranchDev& d = h.dev;
     p.max_p = std::max(p.max_p, h.P);
     if (!d.fused) {
-      p.generic.push_back(b);
-      p.max_p_generic = std::max(p.max_p_generic, h.P);
+      p.gx.push_back(b);
       continue;
     }
     LaunchGroup key;
@@ -215,14 +215,59 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       grp->items.push_back(it);
     }
   }
+  // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
+  std::stable_sort(p.gx.begin(), p.gx.end(),
+                   [&](int32_t a, int32_t b) { return ctx->br[a].gx_group < ctx->br[b].gx_group; });
+  for (size_t i = 0; i < p.gx.size();) {
+    size_t j = i;
+    GxGroup g;
+    int32_t maxL = 2;
+    while (j < p.gx.size() && ctx->br[p.gx[j]].gx_group == ctx->br[p.gx[i]].gx_group) {
+      maxL = std::max(maxL, ctx->br[p.gx[j]].L);
+      g.max_splits = std::max(g.max_splits, ctx->br[p.gx[j]].dev.nsplits);
+      ++j;
+    }
+    g.first = (int32_t)i;
+    g.count = (int32_t)(j - i);
+    std::vector<std::pair<int, int>> order;  // (phase, layer) in launch order
+    order.push_back({GX_FWD0, 0});
+    for (int l = 1; l < maxL - 1; ++l) order.push_back({GX_FWD, l});
+    order.push_back({GX_HEAD, 0});
+    for (int l = maxL - 2; l >= 1; --l) order.push_back({GX_BWD, l});
+    for (int l = maxL - 2; l >= 1; --l) order.push_back({GX_GRAD, l});
+    order.push_back({GX_GRAD0, 0});
+    for (auto& o : order) {
+      GxPhase ph;
+      ph.ph = o.first;
+      ph.l = o.second;
+      if (ph.ph != GX_HEAD) {
+        ph.pre_off = (int32_t)p.gx_pre.size();
+        int64_t tot = 0;
+        p.gx_pre.push_back(0);
+        for (size_t k = i; k < j; ++k) {
+          tot += gx_tiles(ctx->br[p.gx[k]].dev, ph.ph, ph.l, ctx->nfrag);
+          if (tot >= (1ll << 30)) return fail(ctx, BANN_E_SHAPE, "gx phase has too many tiles for one launch");
+          p.gx_pre.push_back((int32_t)tot);
+        }
+        ph.total = (int32_t)tot;
+        if (tot == 0) continue;
+      }
+      g.phases.push_back(ph);
+    }
+    p.gxg.push_back(std::move(g));
+    i = j;
+  }
   if (persistent) {
     p.owns = true;
     CK(dalloc(&p.d_all, 2 * nb));
-    CK(dalloc(&p.d_gen, (int64_t)p.generic.size()));
+    CK(dalloc(&p.d_gx, (int64_t)p.gx.size()));
+    CK(dalloc(&p.d_gxpre, (int64_t)p.gx_pre.size()));
     CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    if (!p.generic.empty())
-      CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+    if (!p.gx.empty()) {
+      CK(hipMemcpyAsync(p.d_gx, p.gx.data(), p.gx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+      CK(hipMemcpyAsync(p.d_gxpre, p.gx_pre.data(), p.gx_pre.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
+    }
     for (auto& g : p.groups) {
       CK(dalloc(&g.d_items, (int64_t)g.items.size()));
       CK(hipMemcpyAsync(g.d_items, g.items.data(), g.items.size() * sizeof(GradItem), hipMemcpyHostToDevice,
@@ -231,11 +276,15 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
   } else {
     p.owns = false;
     p.d_all = ctx->d_list_scr;
-    p.d_gen = ctx->d_gen_scr;
+    p.d_gx = ctx->d_gen_scr;
+    p.d_gxpre = ctx->d_gxpre_scr;
+    if ((int64_t)p.gx_pre.size() > ctx->gxpre_cap) return fail(ctx, BANN_E_STATE, "gx plan scratch overflow");
     CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
-    if (!p.generic.empty())
-      CK(hipMemcpyAsync(p.d_gen, p.generic.data(), p.generic.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+    if (!p.gx.empty()) {
+      CK(hipMemcpyAsync(p.d_gx, p.gx.data(), p.gx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+      CK(hipMemcpyAsync(p.d_gxpre, p.gx_pre.data(), p.gx_pre.size() * sizeof(int32_t), hipMemcpyHostToDevice,
                         ctx->stream));
+    }
     int64_t off = 0;
     for (auto& g : p.groups) {
       if (off + (int64_t)g.items.size() > ctx->items_cap) return fail(ctx, BANN_E_STATE, "work-item scratch overflow");
@@ -259,8 +308,17 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
     else
       launch_fused_grad_fx(ctx->st, g.d_items, ni, g.L, g.act, g.full, write_pred, ctx->stream);
   }
-  if (!p.generic.empty())
-    launch_generic_grad(ctx->st, p.d_gen, (int32_t)p.generic.size(), 0, p.max_p_generic, ctx->stream);
+  // gx branches: scratch group by scratch group (the groups reuse one scratch)
+  for (const auto& g : p.gxg) {
+    const int32_t* bl = p.d_gx + g.first;
+    launch_gx_prep(ctx->st, bl, g.count, ctx->stream);
+    for (const auto& ph : g.phases) {
+      if (ph.ph == GX_HEAD)
+        launch_gx_head(ctx->st, bl, g.count, g.max_splits, ctx->stream);
+      else
+        launch_gx_gemm(ctx->st, ph.ph, ph.l, bl, p.d_gxpre + ph.pre_off, g.count, ph.total, ctx->stream);
+    }
+  }
   CK(hipGetLastError());
   return BANN_OK;
 }
@@ -321,7 +379,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
-                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
+                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart};
   comm_destroy(ctx);
@@ -559,9 +617,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipSetDevice(ctx->device));
   const int64_t n = ctx->n;
   ctx->nfrag = (int32_t)((n + 15) / 16);
-  const int64_t npad = (int64_t)ctx->nfrag * 16;
   // kernel path per branch: fx (widths <= 4, <= 8 chunks), fxl (widths <= 4,
-  // 9..64 chunks), wx (one hidden layer up to 32 x 32, m <= 128), else generic
+  // 9..64 chunks), wx (one hidden layer up to 32 x 32, m <= 128), else gx (layered MFMA GEMMs)
   int64_t total_frags = 0;
   for (auto& h : ctx->br) {
     for (int i = 0; i < h.m; ++i)
@@ -625,6 +682,13 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   }
   int64_t q_off = 0;
   int64_t x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
+  // gx scratch groups: branches in index order until the budget (BANN_GX_SCRATCH_MB,
+  // default 8 GiB) is full; every group reuses the same device scratch
+  const int64_t gx_rows = ntile * 64;
+  int64_t gx_budget = 8192ll << 18;  // floats
+  if (const char* e = getenv("BANN_GX_SCRATCH_MB")) gx_budget = std::max<int64_t>(1, atoll(e)) << 18;
+  int64_t gx_cur = 0, n_gx = 0;
+  int32_t gx_ngroups = 0;
   int32_t max_splits = 1;
   for (size_t b = 0; b < ctx->br.size(); ++b) {
     BranchHost& h = ctx->br[b];
@@ -650,7 +714,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     d.mk_off = mk_off;
     mk_off += h.m;
     d.y_off = (int64_t)b * n;
-    d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item) : 1;
+    // gx: row splits of ~64 tiles (4096 individuals) for the K = n gradient GEMMs
+    d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item)
+                        : (int32_t)((ntile + 63) / 64);
     if (d.fused == 1 && !env_split) d.nsplits = fx_splits;
     if (d.fused == 3) d.nsplits = fxl_splits[(d.nchunks + 7) / 8];
     if (d.fused == 1)  // overflow guard also under the env overrides
@@ -662,21 +728,40 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     max_splits = std::max(max_splits, d.nsplits);
     d.part_off = part_off;
     part_off += (int64_t)d.nsplits * h.P;
-    d.scr_off = scr_off;
-    if (!d.fused) {
+    if (!d.fused) {  // gx scratch (kernels_gx.hip): padded weights, biases, A_l and H_l per layer
+      if (d.widths[h.L - 2] > GX_HEAD_MAXW) return fail(ctx, BANN_E_SHAPE, "summary layer wider than 4096");
+      auto r4 = [](int64_t v) { return (v + 3) & ~3ll; };
       int64_t o = 0;
-      for (int l = 0; l < h.L - 1; ++l) {
-        d.scr_z[l] = (int32_t)o;
-        o += npad * d.widths[l];
-        d.scr_a[l] = (int32_t)o;
-        o += npad * d.widths[l];
-        d.scr_d[l] = (int32_t)o;
-        o += npad * d.widths[l];
+      for (int l = 0; l < h.L; ++l) {
+        d.gx_wld[l] = (int32_t)r4(d.win[l]);
+        d.gx_w[l] = (int32_t)o;
+        o += (int64_t)d.widths[l] * d.gx_wld[l];
       }
-      d.scr_d[h.L - 1] = (int32_t)o;
-      o += npad;
-      if (o >= (1ll << 31)) return fail(ctx, BANN_E_SHAPE, "generic-path scratch too large for one branch");
-      scr_off += o;
+      for (int l = 0; l < h.L - 1; ++l) {
+        d.gx_b[l] = (int32_t)o;
+        o += r4(d.widths[l]);
+      }
+      d.gx_dwo = (int32_t)o;
+      o += 2 * ntile * r4(d.widths[h.L - 2]);
+      d.gx_rss = (int32_t)o;
+      o += r4(2 * ntile);
+      for (int l = 0; l < h.L - 1; ++l) {
+        d.gx_ld[l] = (int32_t)r4(d.widths[l]);
+        d.gx_a[l] = (int32_t)o;
+        o += gx_rows * d.gx_ld[l];
+        d.gx_h[l] = (int32_t)o;
+        o += gx_rows * d.gx_ld[l];
+        if (o >= (1ll << 31)) return fail(ctx, BANN_E_SHAPE, "gx scratch of one branch exceeds 2^31 floats");
+      }
+      if (gx_cur > 0 && gx_cur + o > gx_budget) {  // a new scratch group
+        ++gx_ngroups;
+        gx_cur = 0;
+      }
+      h.gx_group = gx_ngroups;
+      d.scr_off = gx_cur;
+      gx_cur += o;
+      scr_off = std::max(scr_off, gx_cur);
+      ++n_gx;
     }
   }
   ctx->max_splits = max_splits;
@@ -739,6 +824,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_uturn, nb));
   CK(dalloc(&ctx->d_list_scr, 2 * nb));
   CK(dalloc(&ctx->d_gen_scr, nb));
+  ctx->gxpre_cap = (int64_t)(3 * BANN_MAXL) * (n_gx + gx_ngroups + 2);
+  CK(dalloc(&ctx->d_gxpre_scr, ctx->gxpre_cap));
   CK(dalloc(&ctx->d_items_scr, items));
   ctx->items_cap = items;
   // every branch's tile image in ONE batched pack launch (no per-branch sync), the

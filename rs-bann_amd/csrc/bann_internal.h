@@ -26,7 +26,7 @@ struct BranchDev {
   int64_t part_off;   // float offset into the partial-gradient slabs: nsplits x P
   int64_t dig_off;    // byte offset of the MFMA A-operand digits [nchunks][64][16]
   int64_t y_off;      // offset of the target / prediction vectors (b * n)
-  int64_t scr_off;    // float offset into the generic-path scratch
+  int64_t scr_off;    // gx path: float offset of the branch's scratch within its scratch group
   int32_t m;          // markers in the branch
   int32_t nchunks;    // ceil(m / 64)
   int32_t L;          // number of layers (weight matrices)
@@ -34,15 +34,20 @@ struct BranchDev {
   int32_t prior;      // bann_prior
   int32_t P;          // num params
   int32_t nsplits;    // row splits (partial slabs)
-  int32_t fused;      // kernel path: 1 = fx, 3 = fxl (widths <= 4), 2 = wide (wx), 0 = generic
+  int32_t fused;      // kernel path: 1 = fx, 3 = fxl (widths <= 4), 2 = wide (wx), 0 = gx (layered MFMA GEMMs)
   int32_t widths[BANN_MAXL];  // out width of each layer (last = 1)
   int32_t win[BANN_MAXL];     // in width of each layer (win[0] = m)
   int32_t woff[BANN_MAXL];    // param_vec offset of W_l
   int32_t boff[BANN_MAXL];    // param_vec offset of b_l (l < L-1)
-  int32_t scr_z[BANN_MAXL];   // generic scratch: per-layer offsets (x n) of z_l
-  int32_t scr_a[BANN_MAXL];   //   a_l
-  int32_t scr_d[BANN_MAXL];   //   delta_l
-  int32_t scr_stride;         //   floats per individual
+  // gx path scratch (kernels_gx.hip), float offsets from scr_off, every one a multiple of 4
+  int32_t gx_w[BANN_MAXL];    // Wp_l: W_l as [out][gx_wld[l]] rows (layer 0: W0 / sigma)
+  int32_t gx_wld[BANN_MAXL];  //   its row stride: win_l rounded up to 4
+  int32_t gx_b[BANN_MAXL];    // b_l (layer 0: c0 = b0 - mu^T W0 / sigma), l < L-1
+  int32_t gx_a[BANN_MAXL];    // A_l = h(Z_l): [rows][gx_ld[l]], l < L-1
+  int32_t gx_h[BANN_MAXL];    // H_l = h'(Z_l), overwritten by delta_l in the backward
+  int32_t gx_ld[BANN_MAXL];   //   row stride: w_l rounded up to 4
+  int32_t gx_dwo;             // head: f64 dW_out partials [tile][S]
+  int32_t gx_rss;             // head: f64 rss partials [tile]
   // precision coordinates (precision_vec order, params.rs:272-289) for joint HMC
   int64_t q_off;              // offset into the per-precision arrays (phi, ...)
   int32_t nq;                 // num precisions
@@ -83,7 +88,7 @@ struct DevState {
   float* y;               // targets [nbranch][n]
   float* pred;            // predictions [nbranch][n]
   float* pred0;           // predictions at the trajectory start
-  float* scr;             // generic-path scratch
+  float* scr;             // gx-path scratch (one scratch group's worth)
   float* eprec;           // error precision per branch
   double* h0;             // initial -H per branch
   double* htrace;         // [nbranch][Lint+1]
@@ -135,8 +140,14 @@ void launch_pack_tiles(const uint8_t* raw, int64_t rowb, const PackJob* jobs, in
 void launch_gather_stats(const float* mu, const float* sigma, const int32_t* snp_idx, int32_t m, float* mu_b,
                          float* sig_b, hipStream_t s);
 
-void launch_generic_grad(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_m, int32_t max_p,
-                         hipStream_t s);
+// gx: the layered MFMA path (kernels_gx.hip)
+enum { GX_FWD0 = 0, GX_FWD = 1, GX_BWD = 2, GX_GRAD = 3, GX_GRAD0 = 4, GX_HEAD = 5 };
+int64_t gx_tiles(const BranchDev& d, int ph, int l, int32_t nfrag);
+void launch_gx_prep(const DevState& st, const int32_t* blist, int nb, hipStream_t s);
+void launch_gx_head(const DevState& st, const int32_t* blist, int nb, int max_splits, hipStream_t s);
+void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, const int32_t* prefix, int nb,
+                    int total, hipStream_t s);
+#define GX_HEAD_MAXW 4096   // widest summary layer of a gx branch
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
                    hipStream_t s, int large);
 bool update_is_large(const BranchDev& d);  // served by the 1024-thread update kernel

@@ -18,6 +18,7 @@ struct BranchHost {
   std::vector<float> prec;  // precision_vec order
   float ows_reg_sum = 0.f;  // output-weight summary stat of the OTHER branches (joint HMC)
   float ows_num = -1.f;     // output-weight count of the network (< 0: this branch's own)
+  int32_t gx_group = -1;    // gx path: scratch group (branches of one group share no scratch)
   BranchDev dev{};
 };
 
@@ -29,13 +30,26 @@ struct LaunchGroup {
   GradItem* d_items = nullptr;
 };
 
+// gx path (kernels_gx.hip): the GEMM phases of one scratch group, each over a
+// tile-count prefix array of the group's branches
+struct GxPhase {
+  int32_t ph = 0, l = 0, total = 0, pre_off = 0;
+};
+struct GxGroup {
+  int32_t first = 0, count = 0, max_splits = 1;  // branches p.gx[first .. first + count)
+  std::vector<GxPhase> phases;                    // in launch order; GX_HEAD marks the head kernel
+};
+
 struct Plan {
-  std::vector<int32_t> all, generic;
+  std::vector<int32_t> all, gx;
   int32_t n_small = 0, n_large = 0;  // update kernels: d_all[nb .. nb+n_small) small, then n_large large
   std::vector<LaunchGroup> groups;
-  int32_t max_p_generic = 0, max_p = 0;
+  std::vector<GxGroup> gxg;
+  std::vector<int32_t> gx_pre;       // concatenated tile prefix arrays of the gx phases
+  int32_t max_p = 0;
   int32_t* d_all = nullptr;
-  int32_t* d_gen = nullptr;
+  int32_t* d_gx = nullptr;
+  int32_t* d_gxpre = nullptr;
   bool owns = false;
 };
 
@@ -81,7 +95,9 @@ struct bann_ctx {
   int32_t htrace_cap = 0;  // L+1 capacity of d_htrace rows
   // scratch plan buffers (per-call plans)
   int32_t* d_list_scr = nullptr;
-  int32_t* d_gen_scr = nullptr;
+  int32_t* d_gen_scr = nullptr;   // gx branch list of a per-call plan
+  int32_t* d_gxpre_scr = nullptr; // its tile prefix arrays (gxpre_cap ints)
+  int64_t gxpre_cap = 0;
   GradItem* d_items_scr = nullptr;
   unsigned long long* d_dbg = nullptr;  // BANN_STAMPS diagnostics
   int64_t items_cap = 0;

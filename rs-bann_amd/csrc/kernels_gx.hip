@@ -1,0 +1,557 @@
+// kernels_gx.hip — "gx": the layered gradient path for every branch shape the
+// fused single-pass kernels do not take (fx/fxl: every width <= 4; wx: one hidden
+// layer <= 32 x 32 over <= 128 markers): any depth, any widths, any marker count
+// -- among them the reference's default architecture, hidden and summary widths
+// m_b / 2 (cli.rs:365-375, rs-bann.rs:433-435).
+//
+// BranchSampler::backpropagate (branch_sampler.rs:813-875) with forward_feed
+// (743-782) as a chain of batched GEMMs over the branches of one scratch group.
+// Every GEMM runs on the f32 MFMA (v_mfma_f32_16x16x4_f32: f32 products, 64
+// flop/clk/SIMD, the f32 peak), accumulating in f32 inside 64-deep K blocks and
+// in f64 across them, so long reductions (m markers, n individuals) do not grow
+// the f32 error with K:
+//   PREP    Wp_l = W_l as [out][in] rows padded to 4; Wp_0 = W0 / sigma and
+//           c0 = b0 - sum_j mu_j Wp_0[.][j] (f64): standardisation folded into W0
+//   FWD0    Z0 = G Wp_0^T + c0 (G decoded from the 2-bit tile image)   -> A0 = h(Z0), H0 = h'(Z0)
+//   FWD l   Z_l = A_{l-1} Wp_l^T + b_l                                  -> A_l, H_l
+//   HEAD    out = A_s w_out (775-782), e = out - y, rss (823-828), pred,
+//           dW_out = A_s^T e (830-835), delta_s = H_s * e w_out (844-847, in place over H_s)
+//   BWD l   delta_{l-1} = H_{l-1} * (delta_l Wp_l)          (855-861, in place over H_{l-1})
+//   GRAD l  dW_l = A_{l-1}^T delta_l, db_l = 1^T delta_l    (849-852; K = individuals, row splits)
+//   GRAD0   dW0 = (G^T delta0 - mu (1^T delta0)) / sigma, db0 (863-866)
+// Every workgroup computes a 64 x 64 output tile with 4 waves (32 x 32 each, four
+// 16 x 16 accumulators); operands are staged through registers into a
+// double-buffered LDS image [row][k] with 68-float rows (the MFMA's one-float A/B
+// reads -- lane (i, q) at row i, k = 4 s + q -- hit 64 distinct banks).  Tiles are
+// numbered so that consecutive ones share an operand block (the row block of a
+// forward, the row range of a gradient split) and are mapped to ONE XCD, so the
+// shared block is read from HBM once into that XCD's L2.
+//
+// Scratch (per branch, f32, offsets in BranchDev::gx_*): Wp_l, bias_l, A_l and
+// H_l of [rows][ld_l] for every hidden/summary layer, the head's per-tile f64
+// partials, rows = 64 * ntile (rows >= n
+// carry zero genotypes; their error is 0, so they add nothing to any gradient).
+// Gradients go to the branch's partial slabs part[split][P] (reduced in a fixed
+// order by k_update), the rss to rss_part: bitwise reproducible.
+#include "activations.h"
+#include "bann_internal.h"
+#include "kernel_util.h"
+
+#define GX_T 64                // output tile edge, K block depth
+#define GX_LD 68               // LDS row stride (floats)
+#define GX_LDS (GX_T * GX_LD)  // floats per operand block
+#ifndef GX_NBUF
+#define GX_NBUF 1              // LDS stages: 1 = 35 KiB per workgroup (4 per CU), 2 = double-buffered (2 per CU)
+#endif
+
+namespace {
+
+__device__ __forceinline__ int64_t gx_rows(const DevState& st) { return (int64_t)((st.nfrag + 3) / 4) * 64; }
+__device__ __forceinline__ float* gx_base(const DevState& st, const BranchDev& bd) { return st.scr + bd.scr_off; }
+
+// the tile numbering of a phase for one branch (must match gx_tiles on the host)
+__device__ __forceinline__ void gx_dims(const DevState& st, const BranchDev& bd, int ph, int l, int& tmc, int& tnc,
+                                        int& ns) {
+  const int ntile = (st.nfrag + 3) / 4;
+  ns = 1;
+  if (ph == GX_FWD0) {
+    tmc = ntile;
+    tnc = (bd.widths[0] + 63) / 64;
+  } else if (ph == GX_FWD) {
+    tmc = ntile;
+    tnc = (bd.widths[l] + 63) / 64;
+  } else if (ph == GX_BWD) {
+    tmc = ntile;
+    tnc = (bd.widths[l - 1] + 63) / 64;
+  } else if (ph == GX_GRAD) {
+    tmc = (bd.widths[l - 1] + 63) / 64;
+    tnc = (bd.widths[l] + 63) / 64;
+    ns = bd.nsplits;
+  } else {  // GX_GRAD0
+    tmc = bd.nchunks;
+    tnc = (bd.widths[0] + 63) / 64;
+    ns = bd.nsplits;
+  }
+}
+
+// a 64 x 64 block of a row-major f32 matrix M[r][c] (row stride ld, a multiple of
+// 4): element (r, c) of the block = M[r0 + r][c0 + c] when r0 + r < rmax and
+// c0 + c < cmax, else 0.  Thread t holds rows (t + 256 u) >> 4, columns 4 (t & 15).
+struct Blk {
+  v4f v[4];
+};
+__device__ __forceinline__ void blk_load(Blk& s, const float* __restrict__ M, int64_t ld, int64_t r0, int64_t rmax,
+                                         int c0, int cmax) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u;
+    const int64_t r = r0 + (e >> 4);
+    const int c = c0 + 4 * (e & 15);
+    v4f x = {0.f, 0.f, 0.f, 0.f};
+    if (r < rmax && c < cmax) {
+      x = *(const v4f*)(M + r * ld + c);
+      if (c + 1 >= cmax) x.y = 0.f;
+      if (c + 2 >= cmax) x.z = 0.f;
+      if (c + 3 >= cmax) x.w = 0.f;
+    }
+    s.v[u] = x;
+  }
+}
+// LDS [r][c] (the block's rows are the MFMA rows, its columns the K index)
+__device__ __forceinline__ void blk_store(const Blk& s, float* L) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u;
+    *(v4f*)(L + (e >> 4) * GX_LD + 4 * (e & 15)) = s.v[u];
+  }
+}
+// LDS [c][r] (the block's columns are the MFMA rows, its rows the K index)
+__device__ __forceinline__ void blk_store_t(const Blk& s, float* L) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = t + 256 * u;
+    const int r = e >> 4, c = 4 * (e & 15);
+    L[(c + 0) * GX_LD + r] = s.v[u].x;
+    L[(c + 1) * GX_LD + r] = s.v[u].y;
+    L[(c + 2) * GX_LD + r] = s.v[u].z;
+    L[(c + 3) * GX_LD + r] = s.v[u].w;
+  }
+}
+
+// one 1 KiB chunk image (64 marker rows x 64 individuals of one tile; u2t layout,
+// kernels_fx.hip header): thread t holds the dword at byte 4 t -- physical row
+// position pos = t >> 2, i.e. logical marker row 16 w + ((P - 8 (w & 1)) & 15)
+// (w = pos >> 4, P = pos & 15), and individuals 16 dq .. 16 dq + 15 at bits 2 s,
+// dq = (t & 3) ^ (P >= 8 ? 2 : 0) (the swapped 8-byte halves).
+__device__ __forceinline__ uint32_t geno_load(const uint8_t* __restrict__ img) {
+  return *(const uint32_t*)(img + 4 * threadIdx.x);
+}
+__device__ __forceinline__ void geno_pos(int& jl, int& dq) {
+  const int t = threadIdx.x, pos = t >> 2, w = pos >> 4, P = pos & 15;
+  jl = 16 * w + ((P - 8 * (w & 1)) & 15);
+  dq = (t & 3) ^ ((P >> 3) << 1);
+}
+// LDS [individual][marker] (FWD0: individuals are the MFMA rows)
+__device__ __forceinline__ void geno_store_im(uint32_t g, float* L) {
+  int jl, dq;
+  geno_pos(jl, dq);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) L[(16 * dq + s) * GX_LD + jl] = (float)((g >> (2 * s)) & 3u);
+}
+// LDS [marker][individual] (GRAD0: markers are the MFMA rows)
+__device__ __forceinline__ void geno_store_mi(uint32_t g, float* L) {
+  int jl, dq;
+  geno_pos(jl, dq);
+  float* p = L + jl * GX_LD + 16 * dq;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t b = g >> (8 * q);
+    *(v4f*)(p + 4 * q) = v4f{(float)(b & 3u), (float)((b >> 2) & 3u), (float)((b >> 4) & 3u), (float)((b >> 6) & 3u)};
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// the GEMM phases
+// ---------------------------------------------------------------------------
+template <int PH>
+__global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
+    k_gx_gemm(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
+              int total, int per) {
+  __shared__ float As[GX_NBUF][GX_LDS];
+  __shared__ float Bs[GX_NBUF][GX_LDS];
+  __shared__ double cs_s[GX_T];
+  // XCD-aware numbering: workgroup i runs on XCD i % 8, so the logical tiles of
+  // one XCD are the contiguous range [xcd * per, (xcd + 1) * per)
+  const int q = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (q >= total) return;
+  int lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (prefix[mid] <= q) lo = mid;
+    else hi = mid;
+  }
+  const int b = blist[lo];
+  const BranchDev& bd = st.br[b];
+  int tmc, tnc, ns;
+  gx_dims(st, bd, PH, l, tmc, tnc, ns);
+  int r = q - prefix[lo];
+  const int split = r / (tmc * tnc);
+  r -= split * tmc * tnc;
+  const int tm = r / tnc, tn = r % tnc;
+  const int64_t rows = gx_rows(st);
+  float* S = gx_base(st, bd);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int ar = 32 * (wv >> 1), bc = 32 * (wv & 1);
+
+  // K range (in blocks of 64) and the operands of this phase
+  int kb0 = 0, kb1;
+  int64_t kcount;  // valid K
+  const float* Am = nullptr;
+  const float* Bm = nullptr;
+  int64_t lda = 0, ldb = 0;
+  int wi = 0, wo = 0;  // GEMM output M / N extent (rows of the output are individuals for FWD/BWD)
+  const uint8_t* img = st.xu2 + bd.x_off;
+  const int64_t tstride = (int64_t)bd.nchunks * 1024;
+  if constexpr (PH == GX_FWD0) {
+    kcount = bd.m;
+    kb1 = bd.nchunks;
+    Bm = S + bd.gx_w[0];
+    ldb = bd.gx_wld[0];
+    wo = bd.widths[0];
+  } else if constexpr (PH == GX_FWD) {
+    kcount = bd.widths[l - 1];
+    kb1 = (int)((kcount + 63) / 64);
+    Am = S + bd.gx_a[l - 1];
+    lda = bd.gx_ld[l - 1];
+    Bm = S + bd.gx_w[l];
+    ldb = bd.gx_wld[l];
+    wo = bd.widths[l];
+  } else if constexpr (PH == GX_BWD) {
+    kcount = bd.widths[l];
+    kb1 = (int)((kcount + 63) / 64);
+    Am = S + bd.gx_h[l];  // delta_l
+    lda = bd.gx_ld[l];
+    Bm = S + bd.gx_w[l];  // Wp_l [k = out][j = in]: loaded transposed
+    ldb = bd.gx_wld[l];
+    wo = bd.widths[l - 1];
+  } else {  // GRAD / GRAD0: K = the split's rows
+    const int ntile = (st.nfrag + 3) / 4;
+    kb0 = (int)((int64_t)ntile * split / ns);
+    kb1 = (int)((int64_t)ntile * (split + 1) / ns);
+    kcount = rows;
+    if constexpr (PH == GX_GRAD) {
+      Am = S + bd.gx_a[l - 1];
+      lda = bd.gx_ld[l - 1];
+      wi = bd.widths[l - 1];
+      Bm = S + bd.gx_h[l];
+      ldb = bd.gx_ld[l];
+      wo = bd.widths[l];
+    } else {
+      wi = bd.m;
+      Bm = S + bd.gx_h[0];
+      ldb = bd.gx_ld[0];
+      wo = bd.widths[0];
+    }
+  }
+  const bool want_cs = (PH == GX_GRAD0) || (PH == GX_GRAD && tm == 0);
+
+  // stage K block kb into registers
+  Blk ra, rb;
+  uint32_t rg = 0;
+  auto load = [&](int kb) {
+    if constexpr (PH == GX_FWD0) {
+      rg = geno_load(img + (int64_t)tm * tstride + (int64_t)kb * 1024);
+      blk_load(rb, Bm, ldb, 64 * tn, wo, 64 * kb, (int)kcount);
+    } else if constexpr (PH == GX_FWD) {
+      blk_load(ra, Am, lda, 64 * (int64_t)tm, rows, 64 * kb, (int)kcount);
+      blk_load(rb, Bm, ldb, 64 * tn, wo, 64 * kb, (int)kcount);
+    } else if constexpr (PH == GX_BWD) {
+      blk_load(ra, Am, lda, 64 * (int64_t)tm, rows, 64 * kb, (int)kcount);
+      blk_load(rb, Bm, ldb, 64 * kb, (int)kcount, 64 * tn, wo);
+    } else if constexpr (PH == GX_GRAD) {
+      blk_load(ra, Am, lda, 64 * (int64_t)kb, rows, 64 * tm, wi);
+      blk_load(rb, Bm, ldb, 64 * (int64_t)kb, rows, 64 * tn, wo);
+    } else {
+      rg = geno_load(img + (int64_t)kb * tstride + (int64_t)tm * 1024);
+      blk_load(rb, Bm, ldb, 64 * (int64_t)kb, rows, 64 * tn, wo);
+    }
+  };
+  auto store = [&](int buf) {
+    if constexpr (PH == GX_FWD0) {
+      geno_store_im(rg, As[buf]);
+      blk_store(rb, Bs[buf]);
+    } else if constexpr (PH == GX_FWD) {
+      blk_store(ra, As[buf]);
+      blk_store(rb, Bs[buf]);
+    } else if constexpr (PH == GX_BWD) {
+      blk_store(ra, As[buf]);
+      blk_store_t(rb, Bs[buf]);
+    } else if constexpr (PH == GX_GRAD) {
+      blk_store_t(ra, As[buf]);
+      blk_store_t(rb, Bs[buf]);
+    } else {
+      geno_store_mi(rg, As[buf]);
+      blk_store_t(rb, Bs[buf]);
+    }
+  };
+
+  v4f acc[4];
+  double dacc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
+  }
+  // f64 accumulation across K blocks where K is long (m markers, n individuals);
+  // the hidden-layer GEMMs (K = a layer width) keep the f32 MFMA chain
+  constexpr bool F64 = PH != GX_FWD && PH != GX_BWD;
+  double cs = 0.0;  // want_cs: column sum of the B block (delta) over the K range, thread t < 64 = column t
+  if (kb0 < kb1) {
+    load(kb0);
+    store(0);
+  }
+  __syncthreads();
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int buf = GX_NBUF == 1 ? 0 : (kb - kb0) & 1;
+    if (kb + 1 < kb1) load(kb + 1);
+    const float* A = As[buf];
+    const float* B = Bs[buf];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int ko = 4 * s + lq;
+      const float a0 = A[(ar + li) * GX_LD + ko], a1 = A[(ar + 16 + li) * GX_LD + ko];
+      const float b0 = B[(bc + li) * GX_LD + ko], b1 = B[(bc + 16 + li) * GX_LD + ko];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[3], 0, 0, 0);
+    }
+    if (want_cs && t < GX_T) {
+      const float* Br = B + t * GX_LD;
+      float c = 0.f;
+#pragma unroll 16
+      for (int k = 0; k < GX_T; ++k) c += Br[k];
+      cs += (double)c;
+    }
+    if constexpr (F64) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        dacc[x][0] += (double)acc[x].x;
+        dacc[x][1] += (double)acc[x].y;
+        dacc[x][2] += (double)acc[x].z;
+        dacc[x][3] += (double)acc[x].w;
+        acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if (GX_NBUF == 1) __syncthreads();  // every wave is done with the stage before it is refilled
+    if (kb + 1 < kb1) store(GX_NBUF == 1 ? 0 : buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds rows ar + 16 X + 4 lq + y, columns bc + 16 Y + li (acc x = 2 X + Y)
+  if constexpr (PH == GX_FWD0 || PH == GX_FWD) {
+    const int lay = PH == GX_FWD0 ? 0 : l;
+    const float* bias = S + bd.gx_b[lay];
+    float* Ao = S + bd.gx_a[lay];
+    float* Ho = S + bd.gx_h[lay];
+    const int64_t ld = bd.gx_ld[lay];
+    const int act = bd.act;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+      const float bj = bias[j];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        const float z = (F64 ? (float)dacc[x][y] : acc[x][y]) + bj;  // mid_layer_pre_activation: matmul + bias
+        const float a = act_h(z, act);
+        Ao[row * ld + j] = a;
+        Ho[row * ld + j] = act_dh(z, a, act);
+      }
+    }
+  } else if constexpr (PH == GX_BWD) {
+    float* Hd = S + bd.gx_h[l - 1];
+    const int64_t ld = bd.gx_ld[l - 1];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        Hd[row * ld + j] *= acc[x][y];  // delta = h'(z) * (delta_next W^T)
+      }
+    }
+  } else {
+    float* part = st.part + bd.part_off + (int64_t)split * bd.P;
+    const int lay = PH == GX_GRAD ? l : 0;
+    const int win = bd.win[lay];
+    if (PH == GX_GRAD0) {
+      if (t < GX_T) cs_s[t] = cs;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        if (i >= wi) continue;
+        double v = dacc[x][y];
+        if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
+          const float sg = st.sigma[bd.mk_off + i];
+          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_s[bc + 16 * (x & 1) + li]) / (double)sg : 0.0;
+        }
+        part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
+      }
+    }
+    if (tm == 0 && t < GX_T && 64 * tn + t < wo) part[bd.boff[lay] + 64 * tn + t] = (float)cs;  // db_l
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PREP: padded weights, W0 / sigma, c0 = b0 - mu^T (W0 / sigma) (f64), biases
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __restrict__ blist) {
+  const int b = blist[blockIdx.x];
+  const BranchDev& bd = st.br[b];
+  float* S = gx_base(st, bd);
+  const float* th = st.theta + bd.p_off;
+  const float* mu = st.mu + bd.mk_off;
+  const float* sg = st.sigma + bd.mk_off;
+  for (int l = 0; l < bd.L; ++l) {
+    const int win = bd.win[l], wo = bd.widths[l], ld = bd.gx_wld[l];
+    float* Wp = S + bd.gx_w[l];
+    const float* W = th + bd.woff[l];
+    const int64_t tot = (int64_t)wo * ld;
+    for (int64_t e = threadIdx.x; e < tot; e += 256) {
+      const int k = (int)(e / ld), j = (int)(e - (int64_t)k * ld);
+      float v = 0.f;
+      if (j < win) {
+        v = W[(int64_t)k * win + j];
+        if (l == 0) v = sg[j] > 0.f ? v / sg[j] : 0.f;
+      }
+      Wp[e] = v;
+    }
+  }
+  __syncthreads();
+  // c0 (one thread per unit, f64 in marker order) and the other biases
+  {
+    const int m = bd.m, ld = bd.gx_wld[0];
+    const float* Wp = S + bd.gx_w[0];
+    for (int k = threadIdx.x; k < bd.widths[0]; k += 256) {
+      double acc = 0.0;
+      for (int j = 0; j < m; ++j) acc += (double)mu[j] * (double)Wp[(int64_t)k * ld + j];
+      S[bd.gx_b[0] + k] = (float)((double)th[bd.boff[0] + k] - acc);
+    }
+  }
+  for (int l = 1; l < bd.L - 1; ++l)
+    for (int k = threadIdx.x; k < bd.widths[l]; k += 256) S[bd.gx_b[l] + k] = th[bd.boff[l] + k];
+}
+
+// ---------------------------------------------------------------------------
+// HEAD: output neuron, error, rss, predictions, dW_out, delta of the summary layer.
+// grid (row tiles, branches): wave w takes rows w, w + 4, ... of the tile (lanes
+// across the summary units, coalesced), then thread t takes units t, t + 256, ...
+// over the tile's 64 rows.  dW_out and the rss leave per-tile f64 partials in the
+// scratch; k_gx_head_red adds them per split in tile order (deterministic).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __restrict__ blist) {
+  __shared__ float e_s[GX_T];
+  __shared__ double r_s[4];
+  const int b = blist[blockIdx.y];
+  const BranchDev& bd = st.br[b];
+  const int tile = blockIdx.x;
+  if (tile >= (st.nfrag + 3) / 4) return;
+  float* S = gx_base(st, bd);
+  const int sl = bd.L - 2, Sw = bd.widths[sl];
+  const float* A = S + bd.gx_a[sl];
+  float* H = S + bd.gx_h[sl];
+  const int64_t ld = bd.gx_ld[sl];
+  const float* wout = S + bd.gx_w[bd.L - 1];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t r0 = 64 * (int64_t)tile;
+  double rss = 0.0;
+  for (int i = wv; i < GX_T; i += 4) {
+    const int64_t row = r0 + i;
+    const float* a = A + row * ld;
+    double acc = 0.0;
+    for (int k = lane; k < Sw; k += 64) acc += (double)a[k] * (double)wout[k];
+    const float out = (float)wave_sum_d(acc);  // out = A_s w_out (the output layer has no bias)
+    float e = 0.f;
+    if (row < st.n) {
+      e = out - st.y[bd.y_off + row];
+      if (lane == 0) st.pred[bd.y_off + row] = out;
+      rss += (double)e * (double)e;  // lane-uniform: counted once below
+    }
+    if (lane == 0) e_s[i] = e;
+  }
+  if (lane == 0) r_s[wv] = rss;
+  __syncthreads();
+  double* dwo = (double*)(S + bd.gx_dwo) + (int64_t)tile * Sw;
+  for (int k = t; k < Sw; k += 256) {
+    const float wk = wout[k];
+    double d = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < GX_T; ++i) {
+      const float ei = e_s[i];
+      const int64_t o = (r0 + i) * ld + k;
+      d += (double)A[o] * (double)ei;
+      H[o] *= ei * wk;  // delta_s = h'(z_s) * (e w_out^T)
+    }
+    dwo[k] = d;
+  }
+  if (t == 0) ((double*)(S + bd.gx_rss))[tile] = ((r_s[0] + r_s[1]) + r_s[2]) + r_s[3];
+}
+
+// grid (splits, branches): dW_out and rss of each split, tiles in order
+__global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t* __restrict__ blist) {
+  const int b = blist[blockIdx.y];
+  const BranchDev& bd = st.br[b];
+  const int split = blockIdx.x;
+  if (split >= bd.nsplits) return;
+  const int ntile = (st.nfrag + 3) / 4;
+  const int t0 = (int)((int64_t)ntile * split / bd.nsplits), t1 = (int)((int64_t)ntile * (split + 1) / bd.nsplits);
+  const float* S = gx_base(st, bd);
+  const int Sw = bd.widths[bd.L - 2];
+  const double* dwo = (const double*)(S + bd.gx_dwo);
+  float* part = st.part + bd.part_off + (int64_t)split * bd.P + bd.woff[bd.L - 1];
+  for (int k = threadIdx.x; k < Sw; k += 256) {
+    double d = 0.0;
+    for (int tl = t0; tl < t1; ++tl) d += dwo[(int64_t)tl * Sw + k];
+    part[k] = (float)d;
+  }
+  if (threadIdx.x == 0) {
+    const double* rs = (const double*)(S + bd.gx_rss);
+    double r = 0.0;
+    for (int tl = t0; tl < t1; ++tl) r += rs[tl];
+    st.rss_part[(int64_t)b * st.max_splits + split] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+void launch_gx_prep(const DevState& st, const int32_t* blist, int nb, hipStream_t s) {
+  if (nb > 0) hipLaunchKernelGGL(k_gx_prep, dim3(nb), dim3(256), 0, s, st, blist);
+}
+void launch_gx_head(const DevState& st, const int32_t* blist, int nb, int max_splits, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_gx_head, dim3((st.nfrag + 3) / 4, nb), dim3(256), 0, s, st, blist);
+  hipLaunchKernelGGL(k_gx_head_red, dim3(max_splits, nb), dim3(256), 0, s, st, blist);
+}
+void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, const int32_t* prefix, int nb,
+                    int total, hipStream_t s) {
+  if (nb <= 0 || total <= 0) return;
+  const int per = (total + 7) / 8;
+  const dim3 g(8 * per), blk(256);
+  switch (ph) {
+    case GX_FWD0: hipLaunchKernelGGL(k_gx_gemm<GX_FWD0>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
+    case GX_FWD: hipLaunchKernelGGL(k_gx_gemm<GX_FWD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
+    case GX_BWD: hipLaunchKernelGGL(k_gx_gemm<GX_BWD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
+    case GX_GRAD: hipLaunchKernelGGL(k_gx_gemm<GX_GRAD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
+    default: hipLaunchKernelGGL(k_gx_gemm<GX_GRAD0>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
+  }
+}
+
+// tiles of phase (ph, l) for one branch: the numbering of gx_dims above
+int64_t gx_tiles(const BranchDev& d, int ph, int l, int32_t nfrag) {
+  const int64_t ntile = (nfrag + 3) / 4;
+  auto cd = [](int64_t a) { return (a + 63) / 64; };
+  switch (ph) {
+    case GX_FWD0: return ntile * cd(d.widths[0]);
+    case GX_FWD: return (l >= 1 && l < d.L - 1) ? ntile * cd(d.widths[l]) : 0;
+    case GX_BWD: return (l >= 1 && l < d.L - 1) ? ntile * cd(d.widths[l - 1]) : 0;
+    case GX_GRAD: return (l >= 1 && l < d.L - 1) ? cd(d.widths[l - 1]) * cd(d.widths[l]) * d.nsplits : 0;
+    default: return (int64_t)d.nchunks * cd(d.widths[0]) * d.nsplits;
+  }
+}

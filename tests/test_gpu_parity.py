@@ -50,7 +50,7 @@ def test_kat_gradient_gpu(Ctx, prior, fused):
     g = X.T.astype(np.int8)  # raw genotypes; mu = 0, sigma = 1 -> X_std == X
     ctx = build_context(Ctx, g, [dict(snps=[0, 1, 2], branch=br, y=y)], fused=fused,
                         stats=(np.zeros(3), np.ones(3)))
-    assert ctx.kernel_path(0) == ("fused" if fused else "generic")
+    assert ctx.kernel_path(0) == ("fused" if fused else "layered")
     grad, rss = ctx.log_density_gradient(0)
     gw, gb = layer_views(br, grad)
     for l in range(3):
@@ -91,6 +91,15 @@ CONFIGS = [
     dict(n=300, m=577, widths=[4, 1], act="leaky_relu", prior="lasso_base"),
     dict(n=640, m=1536, widths=[2, 3, 4, 1], act="tanh", prior="ridge_ard"),
     dict(n=129, m=3000, widths=[4, 2, 1], act="identity", prior="std_normal"),
+    # gx (layered MFMA GEMMs, any shape): the reference's default architecture
+    # W = S = m_b / 2 (cli.rs:365-375), deep and ragged stacks, partial 64-tiles,
+    # several row splits (n > 4096), a summary layer wider than one 256-thread pass
+    dict(n=1200, m=300, widths=[150, 150, 1], act="tanh", prior="ridge_ard"),
+    dict(n=700, m=500, widths=[250, 250, 1], act="relu", prior="lasso_ard"),
+    dict(n=500, m=200, widths=[100, 70, 40, 1], act="silu", prior="ridge_base"),
+    dict(n=4500, m=130, widths=[65, 65, 1], act="leaky_relu", prior="lasso_base"),
+    dict(n=300, m=40, widths=[300, 1], act="tanh", prior="std_normal"),
+    dict(n=9000, m=77, widths=[33, 5, 1], act="tanh", prior="ridge_ard"),
 ]
 
 
@@ -98,14 +107,14 @@ def expected_path(cfg, fused):
     """the kernel family bann_finalize picks (bann_api.hip)"""
     w, m = cfg["widths"], cfg["m"]
     if not fused:
-        return "generic"
+        return "layered"
     if max(w) <= 4 and m <= 512 and len(w) <= 4:
         return "fused"
     if max(w) <= 4 and m <= 4096 and len(w) <= 4:
         return "fused_large"
     if len(w) == 3 and max(w) <= 32 and m <= 128:
         return "wide"
-    return "generic"
+    return "layered"
 
 
 def make_problem(cfg, seed):
@@ -220,7 +229,7 @@ def test_gradient_deterministic_and_split_invariant(Ctx):
 def test_hmc_step_parity(Ctx, prior, fused, widths):
     """hmc_step (branch_sampler.rs:1192-1299) with injected momentum, step sizes
     and acceptance uniform: same trajectory, -H trace, status and end state
-    (4-wide fused kernel, wide wx kernel, generic kernels)."""
+    (4-wide fused kernel, wide wx kernel, layered (gx) kernels)."""
     rng = np.random.default_rng(11)
     n, m, L = 600, 120, 6
     g = O.synthetic_genotypes(rng, n, m)
@@ -358,6 +367,50 @@ def test_device_step_sizes_match_oracle(Ctx, mode):
         else:
             ref = O.param_vec(*O.izmailov_step_sizes(s["branch"], c, L)).astype(np.float32)
         assert np.allclose(got, ref, rtol=2e-7, atol=0), (priors[k], np.max(np.abs(got / ref - 1)))
+    ctx.close()
+
+
+def test_device_momentum_moments(Ctx):
+    """k_sample_momentum (sample_momentum, branch_sampler.rs:594-609: p ~ N(0, 1)):
+    the device momenta are recovered from the first recorded position step of a
+    trajectory with injected eps = 1e-2 (theta_1 = theta_0 + eps (p + eps/2
+    ldg(theta_0))) and must look standard normal -- mean, variance, kurtosis,
+    KS distance, no lag-1 or cross-branch correlation; the same seed gives the same
+    draws, another seed different ones."""
+    from scipy import stats
+    rng = np.random.default_rng(41)
+    n, m, nb = 300, 256, 8
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = [dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, [4, 4, 1])), y=rng.normal(size=n)) for b in range(nb)]
+    ctx = build_context(Ctx, g, specs)
+    P = ctx.num_params(0)
+    e = 1e-2
+    ctx.set_trajectory_recording(True)
+
+    def draw(seed):
+        th0 = [ctx.get_params(b).astype(np.float64) for b in range(nb)]
+        ldg0 = [ctx.log_density_gradient(b)[0].astype(np.float64) for b in range(nb)]
+        ctx.hmc_step(list(range(nb)), 1, 1e9, eps=np.full(nb * P, e, np.float32), seed=seed, u=np.zeros(nb))
+        ps = []
+        for b in range(nb):
+            th1 = ctx.get_trajectory(b)["params"][0].astype(np.float64)
+            ps.append((th1 - th0[b]) / e - 0.5 * e * ldg0[b])
+            ctx.set_params(b, th0[b].astype(np.float32))   # u = 0 accepts: put the chain back
+        return np.array(ps)
+
+    p = draw(1234)
+    x = p.ravel()
+    N = x.size
+    assert abs(x.mean()) < 4.0 / np.sqrt(N), x.mean()
+    assert abs(x.var() - 1.0) < 4.0 * np.sqrt(2.0 / N), x.var()
+    assert abs(stats.kurtosis(x)) < 4.0 * np.sqrt(24.0 / N)
+    assert stats.kstest(x, "norm").pvalue > 1e-3
+    assert abs(np.corrcoef(x[:-1], x[1:])[0, 1]) < 4.0 / np.sqrt(N)
+    c = np.corrcoef(p)
+    assert np.max(np.abs(c[np.triu_indices(nb, 1)])) < 5.0 / np.sqrt(P)
+    assert np.allclose(draw(1234), p, atol=1e-3)        # same seed: same momenta (recovery error ~1e-5)
+    assert np.max(np.abs(draw(99) - p)) > 1.0           # another seed: other momenta
     ctx.close()
 
 
@@ -530,6 +583,73 @@ def test_c3_shape_branch_parity(Ctx):
     ctx.close()
 
 
+def test_default_arch_full_n(Ctx):
+    """One branch of the reference's default architecture (W = S = m_b / 2,
+    cli.rs:365-375) at the bench cohort's n = 50 000: the gx GEMMs over 782 row
+    tiles, 13 row splits of the gradient GEMMs and 4 column tiles per layer."""
+    n, m = 50_000, 500
+    rng, g, snps, br = make_problem(dict(n=n, m=m, widths=[250, 250, 1], act="tanh", prior="ridge_ard"), 23)
+    ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(n))])
+    assert ctx.kernel_path(0) == "layered"
+    X = oracle_inputs(ctx, g, snps)
+    f = O.predict(br, X)
+    y = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    grad, rss = ctx.log_density_gradient(0)
+    ogw, ogb, orss = O.log_density_gradient(br, X, y)
+    gw, gb = layer_views(br, grad)
+    for l in range(br.num_layers):
+        assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
+    for l in range(br.num_layers - 1):
+        assert norm_rel(gb[l], ogb[l]) < TOL, ("b", l, norm_rel(gb[l], ogb[l]))
+    assert scalar_close(rss, orss), (rss, orss)
+    assert norm_rel(ctx.predict(0), f) < TOL
+    ctx.close()
+
+
+def test_layered_scratch_groups_and_packing(Ctx):
+    """gx branches of mixed shapes in several scratch groups (a 1 MiB budget puts
+    every branch in its own group, so later groups overwrite the scratch of
+    earlier ones): every gradient matches the oracle, equals the one-group
+    result bitwise, and is bitwise reproducible."""
+    rng = np.random.default_rng(29)
+    n, M = 1500, 900
+    g = O.synthetic_genotypes(rng, n, M)
+    shapes = [(300, [150, 150, 1], "tanh", "ridge_ard"), (70, [35, 1], "relu", "lasso_base"),
+              (129, [64, 65, 3, 1], "silu", "ridge_base"), (500, [5, 250, 1], "tanh", "lasso_ard")]
+    specs = []
+    for m, w, a, p in shapes:
+        snps = rng.choice(M, size=m, replace=False).astype(np.int32)
+        br = f32_branch(O.random_branch(rng, m, w, prior=p, act=a))
+        specs.append(dict(snps=snps, branch=br, y=rng.normal(size=n).astype(np.float32).astype(np.float64)))
+    grads = []
+    for budget in ("1", None):
+        if budget:
+            os.environ["BANN_GX_SCRATCH_MB"] = budget
+        try:
+            ctx = build_context(Ctx, g, specs)
+        finally:
+            os.environ.pop("BANN_GX_SCRATCH_MB", None)
+        assert all(ctx.kernel_path(b) == "layered" for b in range(len(specs)))
+        mu, sd = ctx.genotype_stats()
+        res = ctx.predict_many(list(range(len(specs))))
+        gb = []
+        for b, s in enumerate(specs):
+            X = x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]])
+            grad, rss = ctx.log_density_gradient(b)
+            ogw, ogb, orss = O.log_density_gradient(s["branch"], X, s["y"])
+            assert norm_rel(grad, O.param_vec(ogw, ogb)) < TOL, b
+            assert scalar_close(rss, orss)
+            assert norm_rel(res[b], O.predict(s["branch"], X)) < TOL
+            g2, _ = ctx.log_density_gradient(b)
+            assert np.array_equal(grad, g2)
+            gb.append(grad)
+        grads.append(gb)
+        ctx.close()
+    for a, b in zip(*grads):
+        assert np.array_equal(a, b)
+
+
 # ------------------------------------------------------------- wide kernel (wx)
 def _wide_problem(Ctx, seed, n=2000, m=125, widths=(32, 32, 1), nb=3, act="tanh"):
     rng = np.random.default_rng(seed)
@@ -618,7 +738,7 @@ def test_c5_shape_wide_full_n(Ctx):
 HYPER = (0.5, 2.0, 0.8, 3.0, 1.1, 5.0)   # dense, summary, output (shape, scale)
 
 
-@pytest.mark.parametrize("shape", [("fx", 60, [4, 4, 1]), ("wide", 40, [8, 8, 1]), ("generic", 30, [6, 5, 3, 1])])
+@pytest.mark.parametrize("shape", [("fx", 60, [4, 4, 1]), ("wide", 40, [8, 8, 1]), ("layered", 30, [6, 5, 3, 1])])
 @pytest.mark.parametrize("prior", ["ridge_ard", "ridge_base", "lasso_ard", "lasso_base"])
 def test_hmc_step_joint_parity(Ctx, prior, shape):
     """hmc_step_joint (branch_sampler.rs:1070-1178) with injected step sizes,
@@ -633,7 +753,7 @@ def test_hmc_step_joint_parity(Ctx, prior, shape):
     br = f32_branch(O.random_branch(rng, m, widths, prior=prior, act="tanh"))
     br.out_reg_sum, br.out_num_params = float(np.float32(0.37)), 24.0
     ctx = build_context(Ctx, g, [dict(snps=np.arange(m, dtype=np.int32), branch=br, y=np.zeros(n))])
-    assert ctx.kernel_path(0) == {"fx": "fused", "wide": "wide", "generic": "generic"}[path]
+    assert ctx.kernel_path(0) == {"fx": "fused", "wide": "wide", "layered": "layered"}[path]
     ctx.set_output_stats(0, br.out_reg_sum, br.out_num_params)
     X = oracle_inputs(ctx, g, np.arange(m))
     y = (O.predict(br, X) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)

@@ -1,4 +1,4 @@
-"""Acceptance diagnostics for the C5 architecture (W = S = 32, m = 125, n = 100k):
+"""Acceptance diagnostics for the C5 architecture (W = S = 32, m = 125, n = 100k; or M / N / WIDTH):
 status counts and -H drift of bann_hmc_step trajectories at several Izmailov
 factors, on a reduced branch count (same per-branch shape as bench.py --config c5)."""
 import json, math, os, sys
@@ -9,7 +9,9 @@ sys.path.insert(0, ROOT)
 from bann import BannContext
 from bench import init_branch_params
 
-nb, m, n, W = int(os.environ.get("NB", 64)), 125, 100_000, [32, 32, 1]
+nb = int(os.environ.get("NB", 64))
+m, n = int(os.environ.get("M", 125)), int(os.environ.get("N", 100_000))   # c3def: M=500 N=50000 WIDTH=250
+W = [int(os.environ.get("WIDTH", 32))] * 2 + [1]
 L = int(os.environ.get("L", 20))
 ctx = BannContext(0)
 ctx.synthetic_genotypes(n, nb * m, seed=3)
