@@ -105,10 +105,12 @@ def main():
                     help="profiling only: run rank 0's shard of an N-GPU job on this one GPU, no collective")
     ap.add_argument("--hidden-bf16", action="store_true",
                     help="wide kernel: hidden GEMMs on bf16 MFMA (C5's bf16 vs fp32 comparison)")
-    ap.add_argument("--sampler", default="branch", choices=["branch", "network"],
+    ap.add_argument("--sampler", default="branch", choices=["branch", "network", "sequential"],
                     help="branch: every branch's trajectory against the sweep-start residual, one residual "
                          "exchange per trajectory (default); network: one HMC state over all branches, the summed "
-                         "branch outputs all-reduced every leapfrog step (bann_network_hmc_step)")
+                         "branch outputs all-reduced every leapfrog step (bann_network_hmc_step); sequential: the "
+                         "reference's own sweep order, one branch at a time against the refreshed residual "
+                         "(bann_net_train, Net::train net.rs:201-358), one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +210,14 @@ def main():
     residual = noise.astype(np.float32)   # the sweep's residual y - sum_b f_b (net.rs:279-300)
     y_net = (noise + fsum).astype(np.float32)
 
+    net, seen = None, [0.0]
+    if args.sampler == "sequential":
+        if world > 1:
+            raise SystemExit("--sampler sequential is the single-device driver (Net::train)")
+        from bann.net import MCMCConfig, Net
+        net = Net(ctx, seed=5)
+        net.set_global(2.0, float(out_prec))
+
     def trajectory(L, seed):
         """one HMC trajectory of L leapfrog steps.  branch sampler: every branch of
         this rank (momentum draw + initial gradient, L fused steps, Metropolis),
@@ -216,6 +226,11 @@ def main():
         state over all branches of all ranks, the summed outputs all-reduced every
         step (bann_network_hmc_step)."""
         nonlocal residual
+        if args.sampler == "sequential":   # one sweep: every branch one L-step trajectory, in shuffled order
+            net.train(y_net, MCMCConfig(hmc_step_size_factor=args.step_factor, hmc_integration_length=L,
+                                        chain_length=1, burn_in=1))
+            before, seen[0] = seen[0], float(net.summary()["num_accepted"])
+            return seen[0] - before
         if args.sampler == "network":
             r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov",
                                      step_factor=args.step_factor, seed=seed, u=0.5)
@@ -252,7 +267,8 @@ def main():
 
     workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
                 "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else "") +
-                (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else ""))
+                (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else "") +
+                (", sequential Net::train sweep (one branch at a time)" if args.sampler == "sequential" else ""))
     kernel_name = {"wide": "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
                    "layered": "k_gx_gemm"}[path]
     # ---- kernel timing for the roofline (HIP events on the library stream) ----

@@ -29,6 +29,7 @@ void free_plan(Plan& p) {
     dfree(p.d_all);
     dfree(p.d_gx);
     dfree(p.d_gxpre);
+    dfree(p.d_fold);
     for (auto& g : p.groups) dfree(g.d_items);
   }
   p = Plan{};
@@ -178,6 +179,22 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     if (update_is_large(ctx->br[branches[i]].dev)) lists.push_back(branches[i]);
   p.n_large = nb - p.n_small;
   const int64_t nfrag = ctx->nfrag, ntile = (nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
+  // solo mode: too few work items to fill the GPU -> every fused branch re-split
+  // into its solo_items items, partials into the solo region, folded afterwards
+  bool solo = false;
+  {
+    int64_t items = 0, need = 0, need_rss = 0;
+    for (int i = 0; i < nb; ++i) {
+      const BranchHost& h = ctx->br[branches[i]];
+      if (!h.dev.fused) continue;
+      const int spi = h.dev.fused == 2 ? 4 : 1;  // slabs per item
+      items += h.dev.nsplits / spi;
+      need += (int64_t)h.solo_items * spi * h.P;
+      need_rss += (int64_t)h.solo_items * spi;
+    }
+    solo = items > 0 && items < ctx->solo_threshold && need <= ctx->solo_part_cap && need_rss <= ctx->solo_rss_cap;
+  }
+  int64_t solo_part = ctx->part_total, solo_rss = (int64_t)nbr * ctx->max_splits;
   for (int i = 0; i < nb; ++i) {
     const int b = branches[i];
     const BranchHost& h = ctx->br[b];
@@ -205,14 +222,22 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       p.groups.push_back(key);
       grp = &p.groups.back();
     }
-    const int ns = d.fused == 2 ? d.nsplits / 4 : d.nsplits;
+    const int spi = d.fused == 2 ? 4 : 1;  // wx: every wave of an item writes its own slab
+    const int ns = solo ? h.solo_items : d.nsplits / spi;
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
       GradItem it;
       it.branch = b;
       it.split = s;
       it.frag_begin = (int32_t)(BANN_TILE_FRAGS * (ntile * s / ns));
       it.frag_end = (int32_t)std::min<int64_t>(nfrag, BANN_TILE_FRAGS * (ntile * (s + 1) / ns));
+      it.part_at = solo ? solo_part + (int64_t)s * spi * h.P : d.part_off + (int64_t)s * spi * h.P;
+      it.rss_at = solo ? solo_rss + (int64_t)s * spi : (int64_t)b * ctx->max_splits + (int64_t)s * spi;
       grp->items.push_back(it);
+    }
+    if (solo) {
+      p.fold.push_back(FoldJob{b, ns * spi, solo_part, solo_rss});
+      solo_part += (int64_t)ns * spi * h.P;
+      solo_rss += (int64_t)ns * spi;
     }
   }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
@@ -262,6 +287,10 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     CK(dalloc(&p.d_all, 2 * nb));
     CK(dalloc(&p.d_gx, (int64_t)p.gx.size()));
     CK(dalloc(&p.d_gxpre, (int64_t)p.gx_pre.size()));
+    CK(dalloc(&p.d_fold, (int64_t)p.fold.size()));
+    if (!p.fold.empty())
+      CK(hipMemcpyAsync(p.d_fold, p.fold.data(), p.fold.size() * sizeof(FoldJob), hipMemcpyHostToDevice,
+                        ctx->stream));
     CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     if (!p.gx.empty()) {
       CK(hipMemcpyAsync(p.d_gx, p.gx.data(), p.gx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
@@ -278,6 +307,10 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     p.d_all = ctx->d_list_scr;
     p.d_gx = ctx->d_gen_scr;
     p.d_gxpre = ctx->d_gxpre_scr;
+    p.d_fold = ctx->d_fold_scr;
+    if (!p.fold.empty())
+      CK(hipMemcpyAsync(p.d_fold, p.fold.data(), p.fold.size() * sizeof(FoldJob), hipMemcpyHostToDevice,
+                        ctx->stream));
     if ((int64_t)p.gx_pre.size() > ctx->gxpre_cap) return fail(ctx, BANN_E_STATE, "gx plan scratch overflow");
     CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     if (!p.gx.empty()) {
@@ -308,6 +341,7 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
     else
       launch_fused_grad_fx(ctx->st, g.d_items, ni, g.L, g.act, g.full, write_pred, ctx->stream);
   }
+  if (!p.fold.empty()) launch_fold_solo(ctx->st, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
   // gx branches: scratch group by scratch group (the groups reuse one scratch)
   for (const auto& g : p.gxg) {
     const int32_t* bl = p.d_gx + g.first;
@@ -379,7 +413,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
-                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
+                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_fold_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart};
   comm_destroy(ctx);
@@ -765,6 +799,21 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     }
   }
   ctx->max_splits = max_splits;
+  // solo mode (build_plan): ~one tile per wave for a branch alone on the GPU
+  int64_t max_p_fused = 0;
+  for (auto& h : ctx->br) {
+    const BranchDev& d = h.dev;
+    if (!d.fused) continue;
+    max_p_fused = std::max<int64_t>(max_p_fused, h.P);
+    const int64_t per_item = d.fused == 3 ? 1 : 4;  // fxl: all waves on one tile; fx / wx: 4 waves, own tiles
+    h.solo_items = (int32_t)std::max<int64_t>(d.nsplits / (d.fused == 2 ? 4 : 1),
+                                              std::min<int64_t>(2 * cus, (ntile + per_item - 1) / per_item));
+  }
+  ctx->solo_threshold = cus;
+  if (const char* e = getenv("BANN_SOLO")) ctx->solo_threshold = atoi(e) ? cus : 0;  // 0: never re-split
+  ctx->solo_rss_cap = 8ll * cus;
+  ctx->solo_part_cap = ctx->solo_rss_cap * max_p_fused;
+  ctx->part_total = part_off;
   ctx->packed_bytes = x2_off;
   ctx->total_p = p_off;
   ctx->total_q = q_off;
@@ -800,9 +849,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     CK(dalloc(&ctx->d_pidx, p_off));
     CK(hipMemcpy(ctx->d_pidx, pidx.data(), p_off * sizeof(int32_t), hipMemcpyHostToDevice));
   }
-  CK(dalloc(&ctx->d_part, part_off));
+  CK(dalloc(&ctx->d_part, part_off + ctx->solo_part_cap));
   CK(hipMemsetAsync(ctx->d_part, 0, part_off * sizeof(float), ctx->stream));
-  CK(dalloc(&ctx->d_rss_part, nb * max_splits));
+  CK(dalloc(&ctx->d_rss_part, nb * max_splits + ctx->solo_rss_cap));
   CK(hipMemsetAsync(ctx->d_rss_part, 0, nb * max_splits * sizeof(double), ctx->stream));
   CK(dalloc(&ctx->d_y, nb * n));
   CK(hipMemsetAsync(ctx->d_y, 0, nb * n * sizeof(float), ctx->stream));
@@ -824,10 +873,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_uturn, nb));
   CK(dalloc(&ctx->d_list_scr, 2 * nb));
   CK(dalloc(&ctx->d_gen_scr, nb));
+  CK(dalloc(&ctx->d_fold_scr, nb));
   ctx->gxpre_cap = (int64_t)(3 * BANN_MAXL) * (n_gx + gx_ngroups + 2);
   CK(dalloc(&ctx->d_gxpre_scr, ctx->gxpre_cap));
-  CK(dalloc(&ctx->d_items_scr, items));
-  ctx->items_cap = items;
+  CK(dalloc(&ctx->d_items_scr, items + ctx->solo_rss_cap));  // a solo plan has <= solo_rss_cap items
+  ctx->items_cap = items + ctx->solo_rss_cap;
   // every branch's tile image in ONE batched pack launch (no per-branch sync), the
   // marker statistics in one gather, the precision-derived arrays in one copy each
   std::vector<int32_t> allidx;

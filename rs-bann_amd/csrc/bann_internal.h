@@ -55,12 +55,25 @@ struct BranchDev {
   int32_t qbias;              // first bias precision (L-1 of them), then the error precision
 };
 
-// One work item of the fused gradient kernel: a contiguous fragment range of one branch.
+// One work item of the fused gradient kernel: a contiguous fragment range of one
+// branch, and where its partial gradient slab(s) and rss partial(s) go: the
+// branch's own slabs (part_off + split P) or, for plans too small to fill the
+// GPU, the "solo" region after them (folded into the branch's slabs by
+// launch_fold_solo).  wx items own 4 consecutive slabs / rss entries (one per wave).
 struct GradItem {
   int32_t branch;
   int32_t split;
   int32_t frag_begin;
   int32_t frag_end;
+  int64_t part_at;  // float offset in DevState::part of the item's (first) slab
+  int64_t rss_at;   // index in DevState::rss_part of its (first) rss partial
+};
+// solo-mode fold: a branch's ns slabs at part[part] / rss_part[rss] -> its slab 0
+struct FoldJob {
+  int32_t branch;
+  int32_t nslab;
+  int64_t part;
+  int64_t rss;
 };
 
 // Per-branch derived constants of the fused path (rewritten after every position update).
@@ -148,6 +161,7 @@ void launch_gx_head(const DevState& st, const int32_t* blist, int nb, int max_sp
 void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, const int32_t* prefix, int nb,
                     int total, hipStream_t s);
 #define GX_HEAD_MAXW 4096   // widest summary layer of a gx branch
+void launch_fold_solo(const DevState& st, const FoldJob* jobs, int32_t njobs, int32_t max_p, hipStream_t s);
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
                    hipStream_t s, int large);
 bool update_is_large(const BranchDev& d);  // served by the 1024-thread update kernel

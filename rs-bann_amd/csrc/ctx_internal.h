@@ -19,6 +19,7 @@ struct BranchHost {
   float ows_reg_sum = 0.f;  // output-weight summary stat of the OTHER branches (joint HMC)
   float ows_num = -1.f;     // output-weight count of the network (< 0: this branch's own)
   int32_t gx_group = -1;    // gx path: scratch group (branches of one group share no scratch)
+  int32_t solo_items = 1;   // fused path: work items of the branch in a solo-mode plan (~1 tile per wave)
   BranchDev dev{};
 };
 
@@ -46,6 +47,8 @@ struct Plan {
   std::vector<LaunchGroup> groups;
   std::vector<GxGroup> gxg;
   std::vector<int32_t> gx_pre;       // concatenated tile prefix arrays of the gx phases
+  std::vector<FoldJob> fold;         // solo mode: per fused branch, its solo slabs -> its slab 0
+  FoldJob* d_fold = nullptr;
   int32_t max_p = 0;
   int32_t* d_all = nullptr;
   int32_t* d_gx = nullptr;
@@ -98,6 +101,12 @@ struct bann_ctx {
   int32_t* d_gen_scr = nullptr;   // gx branch list of a per-call plan
   int32_t* d_gxpre_scr = nullptr; // its tile prefix arrays (gxpre_cap ints)
   int64_t gxpre_cap = 0;
+  FoldJob* d_fold_scr = nullptr;   // fold jobs of a per-call plan (one per branch)
+  // solo mode: a plan whose fused branches give too few work items to fill the
+  // GPU (e.g. the sequential driver's one-branch trajectories) re-splits them
+  // into solo_items each, writing into the solo region after the branch slabs
+  int64_t part_total = 0, solo_part_cap = 0, solo_rss_cap = 0;
+  int32_t solo_threshold = 256;    // normal work items below which a plan goes solo
   GradItem* d_items_scr = nullptr;
   unsigned long long* d_dbg = nullptr;  // BANN_STAMPS diagnostics
   int64_t items_cap = 0;

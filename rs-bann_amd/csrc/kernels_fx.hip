@@ -589,7 +589,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4_exact(acc[u]), Rl - 153) : 0.f;
   }
   __syncthreads();
-  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+  float* part = st.part + it.part_at;
   float db0[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) db0[k] = (s_hs[0][k] + s_hs[1][k]) + (s_hs[2][k] + s_hs[3][k]);
@@ -631,7 +631,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     }
   }
   if (wave == 0 && lane == 0)
-    st.rss_part[(int64_t)b * st.max_splits + it.split] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
+    st.rss_part[it.rss_at] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
 }
 
 template <int NL, int NCH>
@@ -1038,7 +1038,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- epilogue ----
-  float* part = st.part + bd.part_off + (int64_t)it.split * bd.P;
+  float* part = st.part + it.part_at;
   float db0[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) db0[k] = wave_sum(db[0][k]);
@@ -1061,7 +1061,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < NS; ++q) s_hs[q] = hs[q];
-      st.rss_part[(int64_t)b * st.max_splits + it.split] = rs;
+      st.rss_part[it.rss_at] = rs;
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -516,6 +516,39 @@ void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb,
   hipLaunchKernelGGL(k_fused_const, dim3(nb), dim3(UPD_THREADS), 0, s, st, branches);
 }
 
+// solo-mode fold (build_plan): the nslab partial slabs a solo plan wrote for a
+// branch, summed in slab order into the branch's slab 0; its other slabs and rss
+// partials zeroed, so k_update's fixed-order split reduction sees the same sum
+// grid (parameter blocks of 64, jobs): one thread per parameter, its slabs'
+// loads independent (unrolled), many small blocks so the loads of a few hundred
+// slabs spread over the CUs
+__global__ void __launch_bounds__(64) k_fold_solo(DevState st, const FoldJob* __restrict__ jobs) {
+  const FoldJob j = jobs[blockIdx.y];
+  const BranchDev& bd = st.br[j.branch];
+  const int P = bd.P;
+  float* dst = st.part + bd.part_off;
+  const float* src = st.part + j.part;
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i < P) {
+    float v = 0.f;
+#pragma unroll 16
+    for (int s = 0; s < j.nslab; ++s) v += src[(int64_t)s * P + i];
+    dst[i] = v;
+    for (int s = 1; s < bd.nsplits; ++s) dst[(int64_t)s * P + i] = 0.f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    double r = 0.0;
+    for (int s = 0; s < j.nslab; ++s) r += st.rss_part[j.rss + s];
+    double* rd = st.rss_part + (int64_t)j.branch * st.max_splits;
+    rd[0] = r;
+    for (int s = 1; s < bd.nsplits; ++s) rd[s] = 0.0;
+  }
+}
+
+void launch_fold_solo(const DevState& st, const FoldJob* jobs, int32_t njobs, int32_t max_p, hipStream_t s) {
+  if (njobs > 0) hipLaunchKernelGGL(k_fold_solo, dim3((max_p + 63) / 64, njobs), dim3(64), 0, s, st, jobs);
+}
+
 // momentum ~ N(0, 1) (sample_momentum, branch_sampler.rs:594-609): Box-Muller on Philox
 __global__ void k_sample_momentum(DevState st, const int32_t* __restrict__ blist, uint64_t seed) {
   const int b = blist[blockIdx.y];

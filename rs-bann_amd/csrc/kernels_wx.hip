@@ -455,8 +455,8 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // ---- epilogue: this wave's own partial slab (no cross-wave reduction) ----
-  const int slab = 4 * it.split + wave;
-  float* part = st.part + bd.part_off + (int64_t)slab * bd.P;
+  const int slab = wave;  // the item's 4 slabs: one per wave
+  float* part = st.part + it.part_at + (int64_t)slab * bd.P;
   float db0[WX_MB];
 #pragma unroll
   for (int mb = 0; mb < WX_MB; ++mb) db0[mb] = row_sum(db0a[mb]);
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 1)
       }
     }
   const double rs = wave_sum_d(rss);
-  if (lane == 0) st.rss_part[(int64_t)b * st.max_splits + slab] = rs;
+  if (lane == 0) st.rss_part[it.rss_at + slab] = rs;
 }
 
 template <int BF>

@@ -212,12 +212,13 @@ def test_gradient_deterministic_and_split_invariant(Ctx):
     g2, r2 = ctx.log_density_gradient(0)
     assert np.array_equal(g1, g2) and r1 == r2  # fixed-order reductions: bitwise reproducible
     ctx.close()
-    os.environ["BANN_TARGET_ITEMS"] = "1"      # one split instead of many
+    os.environ["BANN_TARGET_ITEMS"] = "1"      # one split instead of many (a one-branch plan
+    os.environ["BANN_SOLO"] = "0"              # otherwise goes solo: ~one tile per wave)
     try:
         ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=y)])
         g3, r3 = ctx.log_density_gradient(0)
     finally:
-        del os.environ["BANN_TARGET_ITEMS"]
+        del os.environ["BANN_TARGET_ITEMS"], os.environ["BANN_SOLO"]
     assert norm_rel(g3, g1) < 1e-6 and abs(r3 - r1) < 1e-6 * abs(r1)
     ctx.close()
 
