@@ -187,10 +187,9 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     for (int i = 0; i < nb; ++i) {
       const BranchHost& h = ctx->br[branches[i]];
       if (!h.dev.fused) continue;
-      const int spi = h.dev.fused == 2 ? 4 : 1;  // slabs per item
-      items += h.dev.nsplits / spi;
-      need += (int64_t)h.solo_items * spi * h.P;
-      need_rss += (int64_t)h.solo_items * spi;
+      items += h.dev.nsplits;
+      need += (int64_t)h.solo_items * h.P;
+      need_rss += h.solo_items;
     }
     solo = items > 0 && items < ctx->solo_threshold && need <= ctx->solo_part_cap && need_rss <= ctx->solo_rss_cap;
   }
@@ -222,8 +221,8 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       p.groups.push_back(key);
       grp = &p.groups.back();
     }
-    const int spi = d.fused == 2 ? 4 : 1;  // wx: every wave of an item writes its own slab
-    const int ns = solo ? h.solo_items : d.nsplits / spi;
+    const int spi = 1;  // partial slabs per work item
+    const int ns = solo ? h.solo_items : d.nsplits;
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
       GradItem it;
       it.branch = b;
@@ -709,6 +708,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     if (h.dev.fused == 3) ++nfxl[(h.dev.nchunks + 7) / 8];
   }
   const int32_t fx_splits = best_splits(nfx, 2 * (int64_t)cus, 4);  // fx: 2 workgroups of 4 waves per CU, tiles interleaved
+  int64_t nwx = 0;
+  for (auto& h : ctx->br) nwx += h.dev.fused == 2;
+  const int32_t wx_splits = best_splits(nwx, 4 * (int64_t)cus, 1);  // wx: 4 two-wave workgroups per CU, a tile at a time
   int32_t fxl_splits[9] = {};
   for (int nw = 2; nw <= 8; ++nw) {  // fxl: all waves of a workgroup on one tile; LDS- and VGPR-limited residency
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4), 8 / nw));
@@ -753,12 +755,12 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
                         : (int32_t)((ntile + 63) / 64);
     if (d.fused == 1 && !env_split) d.nsplits = fx_splits;
     if (d.fused == 3) d.nsplits = fxl_splits[(d.nchunks + 7) / 8];
+    if (d.fused == 2) d.nsplits = wx_splits;
     if (d.fused == 1)  // overflow guard also under the env overrides
       d.nsplits = std::max<int32_t>(d.nsplits, (int32_t)((ntile + 4 * BANN_MAX_TILES_PER_WAVE - 1) /
                                                          (4 * BANN_MAX_TILES_PER_WAVE)));
     d.nsplits = (int32_t)std::max<int64_t>(1, std::min<int64_t>(d.nsplits, ntile));
     if (d.fused) items += d.nsplits;
-    if (d.fused == 2) d.nsplits *= 4;  // wx: every wave of an item writes its own slab
     max_splits = std::max(max_splits, d.nsplits);
     d.part_off = part_off;
     part_off += (int64_t)d.nsplits * h.P;
@@ -805,8 +807,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     const BranchDev& d = h.dev;
     if (!d.fused) continue;
     max_p_fused = std::max<int64_t>(max_p_fused, h.P);
-    const int64_t per_item = d.fused == 3 ? 1 : 4;  // fxl: all waves on one tile; fx / wx: 4 waves, own tiles
-    h.solo_items = (int32_t)std::max<int64_t>(d.nsplits / (d.fused == 2 ? 4 : 1),
+    const int64_t per_item = d.fused == 1 ? 4 : 1;  // fx: 4 waves on their own tiles; fxl / wx: a tile at a time
+    h.solo_items = (int32_t)std::max<int64_t>(d.nsplits,
                                               std::min<int64_t>(2 * cus, (ntile + per_item - 1) / per_item));
   }
   ctx->solo_threshold = cus;

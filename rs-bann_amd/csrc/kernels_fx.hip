@@ -298,16 +298,30 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     __builtin_amdgcn_s_setprio(1);
 #endif
     {
-      v4u Xc = (v4u)lds_tr8_pair(xs + fo0, xs + fo1);
-      v4i Ac = *reinterpret_cast<const v4i*>(&s_w0[lane * 16]);
+#if BANN_ABLATE & 65536
+      constexpr int FD = 1;  // LDS reads one chunk ahead of their MFMAs
+#else
+      constexpr int FD = 2;  // two chunks ahead: an LDS read's latency exceeds one chunk's 4 MFMAs
+#endif
+      v4u Xq[FD];
+      v4i Aq[FD];
+#pragma unroll
+      for (int c = 0; c < FD; ++c) {
+        Xq[c] = v4u{0u, 0u, 0u, 0u};
+        Aq[c] = v4i{0, 0, 0, 0};
+        if (NCH != 0 || c < nch) {
+          Xq[c] = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+          Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
+        }
+      }
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         if (NCH == 0 && c >= nch) continue;
-        v4u Xn = Xc;
-        v4i An = Ac;
-        if (c + 1 < 8 && (NCH != 0 || c + 1 < nch)) {
-          Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
-          An = *reinterpret_cast<const v4i*>(&s_w0[(c + 1) * 1024 + lane * 16]);
+        const v4u Xc = Xq[c % FD];
+        const v4i Ac = Aq[c % FD];
+        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {
+          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
+          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
         }
         if (more) issue_chunk(tt + NW, sl ^ 1, c);
         // fragment q = field q of every byte, kept in place (x 4^q, folded into the
@@ -328,8 +342,6 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
 #endif
         __builtin_amdgcn_sched_barrier(0);
-        Xc = Xn;
-        Ac = An;
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -502,19 +514,35 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 #pragma unroll
       for (int u = 0; u < PD; ++u)
         wq[u] = (NCH != 0 || u < 4 * nch) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
+      // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
+      auto unpack = [](uint32_t wv) -> v4i {
+#if BANN_ABLATE & 8192
+        return v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u), (int)((wv >> 4) & 0x03030303u),
+                   (int)((wv >> 6) & 0x03030303u)};
+#else
+        return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
+                   (int)((wv >> 6) & 0x03030303u)};
+#endif
+      };
+#if !(BANN_ABLATE & 32768)
+      // window u + 2 is unpacked beside window u's MFMA: the MFMA's B operand was
+      // written two iterations earlier, so no VALU -> MFMA hazard padding per window
+      v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);
+#endif
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
         if (NCH == 0 && u >= 4 * nch) continue;
+#if BANN_ABLATE & 32768
         const uint32_t wv = wq[u % PD];
         if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
-#if BANN_ABLATE & 8192
-        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u),
-                           (int)((wv >> 4) & 0x03030303u), (int)((wv >> 6) & 0x03030303u)};
+        const v4i Bv = unpack(wv);
 #else
-        // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
-        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
-                           (int)((wv >> 6) & 0x03030303u)};
+        const v4i Bv = Bn;
+        Bn = Bn2;
+        if (u + 2 < 32 && (NCH != 0 || u + 2 < 4 * nch)) Bn2 = unpack(wq[(u + 2) % PD]);
+        if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))  // slot of window u, consumed two iterations ago
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
 #endif
 #if BANN_ABLATE & 2
         acc[u] += Bv ^ A;
@@ -1017,14 +1045,28 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 #pragma unroll
       for (int u = 0; u < PD; ++u)
         wq[u] = (FULL || u < 4 * cw) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
+      auto unpack = [](uint32_t wv) -> v4i {
+        return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
+                   (int)((wv >> 6) & 0x03030303u)};
+      };
+#if !(BANN_ABLATE & 32768)
+      v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);  // two windows ahead of their MFMA (as in fx)
+#endif
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
         if (!FULL && u >= 4 * cw) continue;
+#if BANN_ABLATE & 32768
         const uint32_t wv = wq[u % PD];
         if (u + PD < 32 && (FULL || u + PD < 4 * cw))
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
-        const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
-                           (int)((wv >> 6) & 0x03030303u)};
+        const v4i Bv = unpack(wv);
+#else
+        const v4i Bv = Bn;
+        Bn = Bn2;
+        if (u + 2 < 32 && (FULL || u + 2 < 4 * cw)) Bn2 = unpack(wq[(u + 2) % PD]);
+        if (u + PD < 32 && (FULL || u + PD < 4 * cw))
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+#endif
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         // the next tile's first two digit operands, half a backward ahead of their use

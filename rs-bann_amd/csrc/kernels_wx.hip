@@ -5,34 +5,36 @@
 //
 // Replaces BranchSampler::backpropagate (branch_sampler.rs:813-875) with its
 // forward_feed (743-782) and rss (823-828) for every wide branch of a plan in
-// one launch, and writes the same per-slab partials d(rss/2)/d(theta) in
+// one launch, and writes the same per-split partials d(rss/2)/d(theta) in
 // param_vec order (params.rs:700-715) as the 4-wide fx kernel.
 //
-// One WAVE owns a 64-individual tile of one branch (like fx); the four waves of
-// a workgroup take interleaved tiles of one (branch, split) item and each wave
-// writes its OWN partial slab (slab = 4 split + wave), so waves never wait for
-// each other after the prologue.  Per tile:
-//   1. masked layer forward, exact: Z0 = G (W0/sigma) + c0 on
+// One workgroup = TWO waves that share each 64-individual tile of one (branch,
+// split) item; wave h owns half of every layer: hidden units c in [16h, 16h+16)
+// (column blocks mb = 4h .. 4h+3) and summary units s in [16h, 16h+16).  Half
+// the accumulators and operand images per wave keep a wave under 256 registers,
+// so two waves share a SIMD and one wave's VALU phases (activations, digits,
+// conversions) run beside the other's MFMA chains.  Per tile:
+//   1. masked layer forward, exact, own columns: Z0 = G (W0/sigma) + c0 on
 //      v_mfma_i32_16x16x64_i8 (W0/sigma as 4 signed 7-bit digits per column,
-//      8 column blocks of 4; the 2-bit genotype fields are the B operand, kept
-//      in place as in fx).  Lane (g, i) ends with Z0[ind 4i+q][col 4mb+g].
-//   2. hidden GEMM forward Z1^T = W1^T A0^T on MFMA: that Z0 layout IS the B
-//      operand of v_mfma_f32_16x16x4_f32 (K = 4 columns of a block) and, with
-//      the K slots of a lane group read as columns 4j+g, of the bf16
-//      v_mfma_f32_16x16x32_bf16 -- no lane movement.
-//   3. head: A1 = h(Z1 + b1), f = A1 w2 (lane-local + a 4x4 register/lane-group
-//      transpose), e = f - y, delta1 = h'(Z1) e w2.
-//   4. err0 = delta1 W1^T on MFMA (delta1 is in the accumulator layout, which
-//      is again the B operand; the A-operand rows are permuted so the result
+//      the 2-bit genotype fields as the B operand, kept in place as in fx).
+//      Lane (g, i) ends with Z0[ind 4i+q][col 4mb+g].  A0 = h(Z0) -> the A0^T
+//      image in LDS (rows = hidden units).                          barrier
+//   2. hidden GEMM, own summary units: Z1^T = W1^T A0^T on
+//      v_mfma_f32_16x16x4_f32 (K = the 32 hidden units, read from the A0^T
+//      image) or v_mfma_f32_16x16x32_bf16 (opt-in).
+//   3. head: A1 = h(Z1 + b1), the output's partial sum over own units -> LDS;
+//                                                                barrier
+//      f = partial_0 + partial_1 (same order in both waves), e = f - y,
+//      delta1 = h'(Z1) e w2 (own units) -> the delta1^T image.       barrier
+//   4. err0 = delta1 W1^T for own hidden units on MFMA (K = all 32 summary
+//      units from the delta1^T image; A-operand rows permuted so the result
 //      lands in the Z0 layout), delta0 = h'(Z0) err0.
-//   5. dW1 = A0^T delta1 on MFMA (K = individuals): A0^T and delta1^T go through
-//      a wave-private LDS image (b128 rows, conflict-free), read back with the
-//      individuals on the K slots.
-//   6. masked layer backward dW0 = G^T delta0 on v_mfma_i32_16x16x64_i8:
-//      delta0 as 4 digits at a per-tile, per-column power-of-two scale (27
-//      significant bits), transposed to the fx digit image; the unpacked
-//      genotype window is shared by the 8 column blocks; int32 digit sums are
-//      converted to f32 once per tile and window.
+//   5. dW1 (own hidden rows) = A0^T delta1 on MFMA (K = individuals).
+//   6. masked layer backward, own columns: dW0 = G^T delta0 on
+//      v_mfma_i32_16x16x64_i8, delta0 as 4 digits at a per-tile, per-column
+//      power-of-two scale (27 significant bits); the digit image overwrites the
+//      wave's own A0^T rows (no other wave reads them after the first barrier).
+// The two waves write disjoint parts of the item's one partial slab.
 // FP32 (BF = 0): the hidden GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 fmaf
 // chains, the vector rate).  BF16 (BF = 1, opt-in: C5's "bf16 hidden GEMM on
 // MFMA vs fp32"): on v_mfma_f32_16x16x32_bf16, 16x the rate, bf16 operand
@@ -41,25 +43,28 @@
 #include "bann_internal.h"
 #include "kernel_util.h"
 
-#define WX_WAVES 4
-#define WX_MAXCH 2     // <= 128 markers (register budget of the dW0 accumulators)
+#define WX_WAVES 2     // waves per workgroup (the two halves of a tile)
+#define WX_MAXCH 2     // <= 128 markers
 #define WX_MB 8        // column blocks of 4 (W <= 32)
 #define WX_SLOT (WX_MAXCH * 1024)
-#define WX_RS 68       // f32 row stride (floats) of the transposed staging images
+#define WX_RS 68       // f32 row stride (floats) of the transposed images
 #define WX_RSH 72      // bf16 row stride (elements)
-#define WX_STAGE (32 * WX_RS * 4)
+#define WX_IMG (32 * WX_RS * 4)  // bytes of one 32-row transposed image
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
-__device__ __forceinline__ float comb4w(v4i d) {  // sum_d D_d 2^(-7 d)
-  return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
+// 2^7 sum_d D_d 2^(-7 d) from the digit sums of one tile (|D| < 2^19): the
+// pairs D0 2^7 + D1 and D2 2^7 + D3 are exact in int32, two conversions
+__device__ __forceinline__ float comb4p(v4i d) {
+  return (float)((d[0] << 7) + d[1]) + (float)((d[2] << 7) + d[3]) * 0x1p-14f;
 }
 
-// signed digits of V = rint(x 2^e), |V| < 2^25 (see kernels_fx.hip digits4_fx)
+// signed digits of V = rint(x 2^e), |V| < 2^27 (see kernels_fx.hip digits4_fx)
 __device__ __forceinline__ uint32_t digits4_wx(float x, int e) {
   const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
   const uint32_t u = (uint32_t)V;
@@ -119,21 +124,30 @@ __device__ __forceinline__ bf16x8 pack8(const float (&v)[8]) {
   for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
   return r;
 }
+// element q of eight bf16x4 rows as one bf16x8 operand (the K slots j = 0..7)
+__device__ __forceinline__ bf16x8 gather8(const bf16x4 (&r)[8], int q) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = r[j][q];
+  return o;
+}
 
 }  // namespace
 
 template <int ACT, int BF>
-__global__ void __launch_bounds__(64 * WX_WAVES, 1)
+__global__ void __launch_bounds__(64 * WX_WAVES, 2)
     k_fused_grad_wx(DevState st, const GradItem* __restrict__ items, int write_pred) {
-  __shared__ __attribute__((aligned(16))) char s_w0[WX_MAXCH * WX_MB * 1024];
-  __shared__ __attribute__((aligned(16))) char s_x[WX_WAVES][2][WX_SLOT];
-  __shared__ __attribute__((aligned(16))) float s_y[WX_WAVES][2][64];
-  __shared__ __attribute__((aligned(16))) char s_st[WX_WAVES][2][WX_STAGE];
+  __shared__ __attribute__((aligned(16))) char s_w0[WX_MAXCH * WX_MB * 1024];  // W0/sigma digits, all columns
+  __shared__ __attribute__((aligned(16))) char s_x[2][WX_SLOT];               // tile images (double-buffered)
+  __shared__ __attribute__((aligned(16))) float s_y[2][64];
+  __shared__ __attribute__((aligned(16))) char s_a[WX_IMG];   // A0^T (rows = hidden units), then delta0 digits
+  __shared__ __attribute__((aligned(16))) char s_d[WX_IMG];   // delta1^T (rows = summary units)
+  __shared__ __attribute__((aligned(16))) float s_po[2][64];  // the output's partial sum of each half
 
   const GradItem it = items[blockIdx.x];
   const int b = it.branch;
   const BranchDev& bd = st.br[b];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // this wave's half
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
   const int nch = bd.nchunks;
@@ -142,57 +156,41 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 1)
   const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
   const float* th = st.theta + bd.p_off;
 
-  // ---- prologue: W0 digit image -> LDS (shared by the four waves) ----
+  // ---- prologue: W0 digit image -> LDS ----
   for (int t = threadIdx.x; t < nch * WX_MB * 64; t += 64 * WX_WAVES)
     *reinterpret_cast<v4i*>(&s_w0[t * 16]) = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + (int64_t)t * 16);
 
-  // per-lane constants (zero outside the real widths: padded units stay exactly 0)
-  float zs[WX_MB], c0v[WX_MB];
+  // per-lane constants of this half (zero outside the real widths: padded units stay exactly 0)
+  float zs[4], c0v[4], b1v[4], w2v[4];
 #pragma unroll
-  for (int mb = 0; mb < WX_MB; ++mb) {
-    const int c = 4 * mb + g;
-    zs[mb] = c < w0 ? st.fc[b].scale[c] : 0.f;
-    c0v[mb] = c < w0 ? st.fc[b].c0[c] : 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * (4 * h + k) + g;  // own hidden unit of column block 4h + k
+    zs[k] = c < w0 ? st.fc[b].scale[c] : 0.f;
+    c0v[k] = c < w0 ? st.fc[b].c0[c] : 0.f;
+    const int s = 16 * h + 4 * g + k;   // own summary unit of register k
+    b1v[k] = s < S ? th[bd.boff[1] + s] : 0.f;
+    w2v[k] = s < S ? th[bd.woff[2] + s] : 0.f;
   }
-  float b1v[2][4], w2v[2][4];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 16 * nb + 4 * g + r;
-      b1v[nb][r] = s < S ? th[bd.boff[1] + s] : 0.f;
-      w2v[nb][r] = s < S ? th[bd.woff[2] + s] : 0.f;
-    }
   auto W1at = [&](int c, int s) { return (c < w0 && s < S) ? th[bd.woff[1] + s * w0 + c] : 0.f; };
-  // hidden-GEMM operand images of W1 (see the header comment for the maps)
-  float wf[2][WX_MB], we[2][2][4];
-  bf16x8 wfb[2], web[2];
+  // hidden-GEMM operands: wf = W1^T rows of own summary units (K = hidden unit
+  // 4 mb + g); we = W1 rows permuted so err0 lands in the Z0 layout of own blocks
+  float wf[WX_MB], we[2][4];
+  bf16x8 wfb, web;
   if constexpr (BF) {
+    float v[8];
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      float v[8];
+    for (int j = 0; j < 8; ++j) v[j] = W1at(4 * j + g, 16 * h + i);
+    wfb = pack8(v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = W1at(4 * j + g, 16 * nb + i);
-      wfb[nb] = pack8(v);
-    }
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = W1at(4 * (4 * cb + (i & 3)) + (i >> 2), 16 * (j >> 2) + 4 * g + (j & 3));
-      web[cb] = pack8(v);
-    }
+    for (int j = 0; j < 8; ++j) v[j] = W1at(4 * (4 * h + (i & 3)) + (i >> 2), 16 * (j >> 2) + 4 * g + (j & 3));
+    web = pack8(v);
   } else {
+#pragma unroll
+    for (int mb = 0; mb < WX_MB; ++mb) wf[mb] = W1at(4 * mb + g, 16 * h + i);
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-      for (int mb = 0; mb < WX_MB; ++mb) wf[nb][mb] = W1at(4 * mb + g, 16 * nb + i);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) we[cb][nb][r] = W1at(4 * (4 * cb + (i & 3)) + (i >> 2), 16 * nb + 4 * g + r);
+      for (int r = 0; r < 4; ++r) we[nb][r] = W1at(4 * (4 * h + (i & 3)) + (i >> 2), 16 * nb + 4 * g + r);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -204,240 +202,241 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 1)
   const int pe = i, po = (i + 8) & 15;
   const uint32_t boe = (uint32_t)(pe * 16 + 4 * (2 * ((g >> 1) ^ (pe >> 3)) + (g & 1)));
   const uint32_t boo = (uint32_t)(po * 16 + 4 * (2 * ((g >> 1) ^ (po >> 3)) + (g & 1)));
-  const int iota = 4 * i + g;  // this lane's own individual within the tile
-  char* const sA = &s_st[wave][0][0];  // A0^T staging, later the delta0 digit image
-  char* const sD = &s_st[wave][1][0];  // delta1^T staging
-  char* const sd_w = sA + (i >> 2) * 256 + (4 * g + (i & 3)) * 16;
-  const char* const sd_r = sA + g * 256 + tq * 16 + 8 * tp;
+  const int iota = 4 * i + g;  // this lane's own individual within the tile (head)
+  // delta0 digit image (4 KiB): f32 mode -- the wave's own A0^T rows (hidden units
+  // 16h .. 16h+15, which only this wave reads after the A0^T barrier); bf16 mode --
+  // behind the half-size bf16 images (wave 0 in s_a, wave 1 in s_d)
+  char* const sdig = BF ? (h == 0 ? s_a : s_d) + 32 * WX_RSH * 2 : s_a + 16 * h * WX_RS * 4;
+  char* const sd_w = sdig + (i >> 2) * 256 + (4 * g + (i & 3)) * 16;
+  const char* const sd_r = sdig + g * 256 + tq * 16 + 8 * tp;
   const float* ybr = st.y + bd.y_off;
   float* predb = st.pred + bd.y_off;
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
-  auto issue_chunk = [&](int tt, int sl, int c) {
-    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
-  };
-  auto issue_y = [&](int tt, int sl) {
-    const int64_t row = 64 * (int64_t)tt + iota;
-    glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
+  // wave h streams chunk h of the next tile (and wave 0 its targets)
+  auto issue_tile = [&](int tt, int sl) {
+    if (h < nch) glds16(xsrc + (int64_t)tt * tile_bytes + h * 1024, &s_x[sl][h * 1024]);
+    if (h == 0) {
+      const int64_t row = 64 * (int64_t)tt + iota;
+      glds4(ybr + (row < n ? row : n - 1), &s_y[sl][0]);
+    }
   };
 
-  // ---- accumulators ----
-  float dW0a[4 * WX_MAXCH][WX_MB];
+  // ---- accumulators (own half) ----
+  float dW0a[4 * WX_MAXCH][4];
 #pragma unroll
   for (int u = 0; u < 4 * WX_MAXCH; ++u)
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb) dW0a[u][mb] = 0.f;
-  float db0a[WX_MB], db1a[2][4], dW2a[2][4];
-  v4f dW1a[2][2];
+    for (int k = 0; k < 4; ++k) dW0a[u][k] = 0.f;
+  float db0a[4], db1a[4], dW2a[4];
 #pragma unroll
-  for (int mb = 0; mb < WX_MB; ++mb) db0a[mb] = 0.f;
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) db1a[nb][r] = dW2a[nb][r] = 0.f;
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb) dW1a[cb][sb] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < 4; ++k) db0a[k] = db1a[k] = dW2a[k] = 0.f;
+  v4f dW1a[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
   double rss = 0.0;
 
-  int tt = tb + wave, sl = 0;
-  if (tt < te) {
-    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
-    issue_y(tt, 0);
-  }
-  for (; tt < te; tt += WX_WAVES, sl ^= 1) {
-    const bool more = tt + WX_WAVES < te;
+  int tt = tb, sl = 0;
+  if (tt < te) issue_tile(tt, 0);
+  for (; tt < te; ++tt, sl ^= 1) {
+    const bool more = tt + 1 < te;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const char* xs = &s_x[wave][sl][0];
+    __syncthreads();  // both chunks and the targets landed; the previous tile's images are consumed
+    if (more) issue_tile(tt + 1, sl ^ 1);
+    const char* xs = &s_x[sl][0];
 
-    // ---- 1. masked layer forward (exact int32 over the chunks) ----
-    float z0[WX_MB][4], a0[WX_MB][4];
+    // ---- 1. masked layer forward, own column blocks (exact int32 over the chunks) ----
+    float z0[4][4], a0[4][4];
     {
-      v4i fa[WX_MB][4];
+      v4i fa[4][4];
 #pragma unroll
-      for (int mb = 0; mb < WX_MB; ++mb)
+      for (int k = 0; k < 4; ++k)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) fa[mb][q] = v4i{0, 0, 0, 0};
+        for (int q = 0; q < 4; ++q) fa[k][q] = v4i{0, 0, 0, 0};
 #pragma unroll
       for (int c = 0; c < WX_MAXCH; ++c) {
         if (c < nch) {
-          if (more) issue_chunk(tt + WX_WAVES, sl ^ 1, c);
           const v4u X = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
           const v4i B0 = (v4i)(X & 0x03030303u);
           const v4i B1 = (v4i)(X & 0x0C0C0C0Cu);
           const v4i B2 = (v4i)(X & 0x30303030u);
           const v4i B3 = (v4i)((X >> 2u) & 0x30303030u);
 #pragma unroll
-          for (int mb = 0; mb < WX_MB; ++mb) {
-            const v4i A = *reinterpret_cast<const v4i*>(&s_w0[((c * WX_MB + mb) * 64 + lane) * 16]);
-            fa[mb][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B0, fa[mb][0], 0, 0, 0);
-            fa[mb][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, fa[mb][1], 0, 0, 0);
-            fa[mb][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B2, fa[mb][2], 0, 0, 0);
-            fa[mb][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B3, fa[mb][3], 0, 0, 0);
+          for (int k = 0; k < 4; ++k) {
+            const v4i A = *reinterpret_cast<const v4i*>(&s_w0[((c * WX_MB + 4 * h + k) * 64 + lane) * 16]);
+            fa[k][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B0, fa[k][0], 0, 0, 0);
+            fa[k][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, fa[k][1], 0, 0, 0);
+            fa[k][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B2, fa[k][2], 0, 0, 0);
+            fa[k][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B3, fa[k][3], 0, 0, 0);
           }
         }
       }
 #pragma unroll
-      for (int mb = 0; mb < WX_MB; ++mb) {
-        z0[mb][0] = zs[mb] * comb4w(fa[mb][0]) + c0v[mb];
-        z0[mb][1] = (0.25f * zs[mb]) * comb4w(fa[mb][1]) + c0v[mb];
-        z0[mb][2] = (0.0625f * zs[mb]) * comb4w(fa[mb][2]) + c0v[mb];
-        z0[mb][3] = (0.0625f * zs[mb]) * comb4w(fa[mb][3]) + c0v[mb];
+      for (int k = 0; k < 4; ++k) {
+        // comb4p carries 2^7; fields 1-3 stay in place (x 4, x 16, x 16)
+        z0[k][0] = (0x1p-7f * zs[k]) * comb4p(fa[k][0]) + c0v[k];
+        z0[k][1] = (0x1p-9f * zs[k]) * comb4p(fa[k][1]) + c0v[k];
+        z0[k][2] = (0x1p-11f * zs[k]) * comb4p(fa[k][2]) + c0v[k];
+        z0[k][3] = (0x1p-11f * zs[k]) * comb4p(fa[k][3]) + c0v[k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a0[mb][q] = act_h_t<ACT>(z0[mb][q]);
+        for (int q = 0; q < 4; ++q) a0[k][q] = act_h_t<ACT>(z0[k][q]);
       }
     }
-    // A0^T -> LDS rows c = 4mb + g, individuals 4i .. 4i+3
+    // own A0^T rows c = 4 (4h + k) + g, individuals 4i .. 4i+3
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb) {
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * (4 * h + k) + g;
       if constexpr (BF) {
-        bf16x4 h4 = {(__bf16)a0[mb][0], (__bf16)a0[mb][1], (__bf16)a0[mb][2], (__bf16)a0[mb][3]};
-        *reinterpret_cast<bf16x4*>(sA + ((4 * mb + g) * WX_RSH + 4 * i) * 2) = h4;
+        bf16x4 h4 = {(__bf16)a0[k][0], (__bf16)a0[k][1], (__bf16)a0[k][2], (__bf16)a0[k][3]};
+        *reinterpret_cast<bf16x4*>(s_a + (c * WX_RSH + 4 * i) * 2) = h4;
       } else {
-        *reinterpret_cast<v4f*>(sA + ((4 * mb + g) * WX_RS + 4 * i) * 4) =
-            v4f{a0[mb][0], a0[mb][1], a0[mb][2], a0[mb][3]};
+        *reinterpret_cast<v4f*>(s_a + (c * WX_RS + 4 * i) * 4) = v4f{a0[k][0], a0[k][1], a0[k][2], a0[k][3]};
       }
     }
+    LDS_BARRIER();  // the full A0^T image
 
-    // ---- 2. hidden GEMM forward: Z1^T = W1^T A0^T ----
-    v4f z1[2][4];
+    // ---- 2. hidden GEMM, own summary units: Z1^T = W1^T A0^T (K = 32 hidden units) ----
+    v4f z1[4];
+    if constexpr (BF) {
+      bf16x4 ra[8];
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+      for (int j = 0; j < 8; ++j) ra[j] = *reinterpret_cast<const bf16x4*>(s_a + ((4 * j + g) * WX_RSH + 4 * i) * 2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        z1[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb, gather8(ra, q), v4f{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    } else {
+      v4f ra[WX_MB];
+#pragma unroll
+      for (int mb = 0; mb < WX_MB; ++mb) ra[mb] = *reinterpret_cast<const v4f*>(s_a + ((4 * mb + g) * WX_RS + 4 * i) * 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-        if constexpr (BF) {
-          float v[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = a0[j][q];
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfb[nb], pack8(v), acc, 0, 0, 0);
-        } else {
-#pragma unroll
-          for (int mb = 0; mb < WX_MB; ++mb) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[nb][mb], a0[mb][q], acc, 0, 0, 0);
-        }
-        z1[nb][q] = acc;
+        for (int mb = 0; mb < WX_MB; ++mb) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[mb], ra[mb][q], acc, 0, 0, 0);
+        z1[q] = acc;
       }
+    }
 
-    // ---- 3. head ----
-    float a1[2][4][4];
-    float p[4];
+    // ---- 3. head: lane (g, i) register r of z1[q] = Z1[s = 16h + 4g + r][ind 4i + q] ----
+    float a1[4][4], p[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) p[q] = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      p[q] = 0.f;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          z1[nb][q][r] += b1v[nb][r];
-          a1[nb][q][r] = act_h_t<ACT>(z1[nb][q][r]);
-          p[q] = fmaf(a1[nb][q][r], w2v[nb][r], p[q]);
-        }
-    xpose4f(p[0], p[1], p[2], p[3]);  // lane L: partials of individual 4i + (L >> 4) from the 4 groups
-    const float out = (p[0] + p[1]) + (p[2] + p[3]);
+      for (int r = 0; r < 4; ++r) {
+        z1[q][r] += b1v[r];
+        a1[q][r] = act_h_t<ACT>(z1[q][r]);
+        p[q] = fmaf(a1[q][r], w2v[r], p[q]);
+      }
+    }
+    xpose4f(p[0], p[1], p[2], p[3]);  // lane L: partials of individual iota from the 4 groups
+    s_po[h][lane] = (p[0] + p[1]) + (p[2] + p[3]);
+    LDS_BARRIER();  // both halves' partial outputs
+    const float out = s_po[0][lane] + s_po[1][lane];
     const int64_t row = 64 * (int64_t)tt + iota;
     const bool valid = row < n;
-    const float yv = s_y[wave][sl][lane];
-    if (more) issue_y(tt + WX_WAVES, sl ^ 1);
+    const float yv = s_y[sl][lane];
     const float e = valid ? out - yv : 0.f;
-    if (write_pred && valid) predb[row] = out;
+    if (h == 0 && write_pred && valid) predb[row] = out;
     rss += (double)e * (double)e;
     float eq[4] = {e, e, e, e};
     xpose4f(eq[0], eq[1], eq[2], eq[3]);  // eq[q] = e of individual 4i + q
-    float d1[2][4][4];
+    float d1[4][4];
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+    for (int r = 0; r < 4; ++r) {
+      float sw = 0.f, sd = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sw = 0.f, sd = 0.f;
+      for (int q = 0; q < 4; ++q) {
+        d1[q][r] = act_dh_t<ACT>(z1[q][r], a1[q][r]) * (eq[q] * w2v[r]);
+        sw = fmaf(a1[q][r], eq[q], sw);
+        sd += d1[q][r];
+      }
+      dW2a[r] += sw;
+      db1a[r] += sd;
+      // delta1^T row s = 16h + 4g + r, individuals 4i .. 4i+3
+      const int s = 16 * h + 4 * g + r;
+      if constexpr (BF) {
+        bf16x4 h4 = {(__bf16)d1[0][r], (__bf16)d1[1][r], (__bf16)d1[2][r], (__bf16)d1[3][r]};
+        *reinterpret_cast<bf16x4*>(s_d + (s * WX_RSH + 4 * i) * 2) = h4;
+      } else {
+        *reinterpret_cast<v4f*>(s_d + (s * WX_RS + 4 * i) * 4) = v4f{d1[0][r], d1[1][r], d1[2][r], d1[3][r]};
+      }
+    }
+    LDS_BARRIER();  // the full delta1^T image
+
+    // ---- 4. err0 = delta1 W1^T for own hidden units (result in the Z0 layout), delta0 ----
+    float d0[4][4];
+    {
+      v4f acc[4];
+      if constexpr (BF) {
+        bf16x4 rd[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          rd[j] = *reinterpret_cast<const bf16x4*>(s_d + ((16 * (j >> 2) + 4 * g + (j & 3)) * WX_RSH + 4 * i) * 2);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(web, gather8(rd, q), v4f{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      } else {
+        v4f rd[2][4];
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rd[nb][r] = *reinterpret_cast<const v4f*>(s_d + ((16 * nb + 4 * g + r) * WX_RS + 4 * i) * 4);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          d1[nb][q][r] = act_dh_t<ACT>(z1[nb][q][r], a1[nb][q][r]) * (eq[q] * w2v[nb][r]);
-          sw = fmaf(a1[nb][q][r], eq[q], sw);
-          sd += d1[nb][q][r];
-        }
-        dW2a[nb][r] += sw;
-        db1a[nb][r] += sd;
-        // delta1^T -> LDS row s = 16 nb + 4 g + r, individuals 4i .. 4i+3
-        if constexpr (BF) {
-          bf16x4 h4 = {(__bf16)d1[nb][0][r], (__bf16)d1[nb][1][r], (__bf16)d1[nb][2][r], (__bf16)d1[nb][3][r]};
-          *reinterpret_cast<bf16x4*>(sD + ((16 * nb + 4 * g + r) * WX_RSH + 4 * i) * 2) = h4;
-        } else {
-          *reinterpret_cast<v4f*>(sD + ((16 * nb + 4 * g + r) * WX_RS + 4 * i) * 4) =
-              v4f{d1[nb][0][r], d1[nb][1][r], d1[nb][2][r], d1[nb][3][r]};
-        }
-      }
-
-    // ---- 4. err0 = delta1 W1^T (result in the Z0 layout), delta0 ----
-    float d0[WX_MB][4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        v4f acc = v4f{0.f, 0.f, 0.f, 0.f};
-        if constexpr (BF) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = d1[j >> 2][q][j & 3];
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(web[cb], pack8(v), acc, 0, 0, 0);
-        } else {
+          v4f a = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(we[cb][nb][r], d1[nb][q][r], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int mb = 4 * cb + r;
-          d0[mb][q] = act_dh_t<ACT>(z0[mb][q], a0[mb][q]) * acc[r];
+            for (int r = 0; r < 4; ++r) a = __builtin_amdgcn_mfma_f32_16x16x4f32(we[nb][r], rd[nb][r][q], a, 0, 0, 0);
+          acc[q] = a;
         }
       }
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb) db0a[mb] += (d0[mb][0] + d0[mb][1]) + (d0[mb][2] + d0[mb][3]);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d0[k][q] = act_dh_t<ACT>(z0[k][q], a0[k][q]) * acc[q][k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db0a[k] += (d0[k][0] + d0[k][1]) + (d0[k][2] + d0[k][3]);
 
-    // ---- 5. dW1 = A0^T delta1 (K = individuals, from the LDS images) ----
+    // ---- 5. dW1 rows c = 16h + 4g + r: A0^T delta1 (K = individuals, from the images) ----
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+    for (int sb = 0; sb < 2; ++sb) {
+      if constexpr (BF) {
 #pragma unroll
-      for (int sb = 0; sb < 2; ++sb) {
-        if constexpr (BF) {
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 A = *reinterpret_cast<const bf16x8*>(s_a + ((16 * h + i) * WX_RSH + 32 * ks + 8 * g) * 2);
+          const bf16x8 B = *reinterpret_cast<const bf16x8*>(s_d + ((16 * sb + i) * WX_RSH + 32 * ks + 8 * g) * 2);
+          dW1a[sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, dW1a[sb], 0, 0, 0);
+        }
+      } else {
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const bf16x8 A = *reinterpret_cast<const bf16x8*>(sA + ((16 * cb + i) * WX_RSH + 32 * ks + 8 * g) * 2);
-            const bf16x8 B = *reinterpret_cast<const bf16x8*>(sD + ((16 * sb + i) * WX_RSH + 32 * ks + 8 * g) * 2);
-            dW1a[cb][sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, dW1a[cb][sb], 0, 0, 0);
-          }
-        } else {
+        for (int t4 = 0; t4 < 4; ++t4) {
+          const v4f A = *reinterpret_cast<const v4f*>(s_a + ((16 * h + i) * WX_RS + 16 * g + 4 * t4) * 4);
+          const v4f B = *reinterpret_cast<const v4f*>(s_d + ((16 * sb + i) * WX_RS + 16 * g + 4 * t4) * 4);
 #pragma unroll
-          for (int t4 = 0; t4 < 4; ++t4) {
-            const v4f A = *reinterpret_cast<const v4f*>(sA + ((16 * cb + i) * WX_RS + 16 * g + 4 * t4) * 4);
-            const v4f B = *reinterpret_cast<const v4f*>(sD + ((16 * sb + i) * WX_RS + 16 * g + 4 * t4) * 4);
-#pragma unroll
-            for (int e4 = 0; e4 < 4; ++e4)
-              dW1a[cb][sb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[e4], B[e4], dW1a[cb][sb], 0, 0, 0);
-          }
+          for (int e4 = 0; e4 < 4; ++e4) dW1a[sb] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[e4], B[e4], dW1a[sb], 0, 0, 0);
         }
       }
+    }
 
-    // ---- 6. delta0 digits (per-tile, per-column scale), masked layer backward ----
-    int R[WX_MB];
+    // ---- 6. delta0 digits (per-tile, per-column scale) over the own A0^T rows, masked backward ----
+    float sc[4];
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb) {
-      const uint32_t mx = row_max_u(max(max(fbits(d0[mb][0]) & 0x7FFFFFFFu, fbits(d0[mb][1]) & 0x7FFFFFFFu),
-                                        max(fbits(d0[mb][2]) & 0x7FFFFFFFu, fbits(d0[mb][3]) & 0x7FFFFFFFu)));
-      R[mb] = (int)((mx >> 23) & 0xFFu) + 2;  // |delta0| < 2^(R - 128): digits carry 27 bits
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t mx = row_max_u(max(max(fbits(d0[k][0]) & 0x7FFFFFFFu, fbits(d0[k][1]) & 0x7FFFFFFFu),
+                                        max(fbits(d0[k][2]) & 0x7FFFFFFFu, fbits(d0[k][3]) & 0x7FFFFFFFu)));
+      const int R = (int)((mx >> 23) & 0xFFu) + 2;  // |delta0| < 2^(R - 128): digits carry 27 bits
+      sc[k] = __builtin_amdgcn_ldexpf(1.f, R - 139);  // comb4p carries 2^7
       uint32_t dq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dq[q] = digits4_wx(d0[mb][q], 153 - R[mb]);
-      xpose4(dq[0], dq[1], dq[2], dq[3]);  // lane L: the 4 columns of block mb for individual iota
-      // (the A0^T image in sA was consumed by step 5 above: in-order LDS per wave)
-      *reinterpret_cast<v4u*>(sd_w + mb * 1024) = v4u{dq[0], dq[1], dq[2], dq[3]};
+      for (int q = 0; q < 4; ++q) dq[q] = digits4_wx(d0[k][q], 153 - R);
+      xpose4(dq[0], dq[1], dq[2], dq[3]);  // lane L: the 4 columns of block 4h + k for individual iota
+      *reinterpret_cast<v4u*>(sd_w + k * 1024) = v4u{dq[0], dq[1], dq[2], dq[3]};
     }
-    v4i Ab[WX_MB];
+    v4i Ab[4];
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb) Ab[mb] = lds_tr8_pair(sd_r + mb * 1024, sd_r + mb * 1024 + 8 * 16);
+    for (int k = 0; k < 4; ++k) Ab[k] = lds_tr8_pair(sd_r + k * 1024, sd_r + k * 1024 + 8 * 16);
 #pragma unroll
     for (int u = 0; u < 4 * WX_MAXCH; ++u) {
       if (u < 4 * nch) {
@@ -445,60 +444,55 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 1)
         const v4i Bv = v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u), (int)((wv >> 4) & 0x03030303u),
                            (int)((wv >> 6) & 0x03030303u)};
 #pragma unroll
-        for (int mb = 0; mb < WX_MB; ++mb) {
-          const v4i t = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ab[mb], Bv, v4i{0, 0, 0, 0}, 0, 0, 0);
-          dW0a[u][mb] = fmaf(comb4w(t), __builtin_amdgcn_ldexpf(1.f, R[mb] - 132), dW0a[u][mb]);
+        for (int k = 0; k < 4; ++k) {
+          const v4i t = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ab[k], Bv, v4i{0, 0, 0, 0}, 0, 0, 0);
+          dW0a[u][k] = fmaf(comb4p(t), sc[k], dW0a[u][k]);
         }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // ---- epilogue: this wave's own partial slab (no cross-wave reduction) ----
-  const int slab = wave;  // the item's 4 slabs: one per wave
-  float* part = st.part + it.part_at + (int64_t)slab * bd.P;
-  float db0[WX_MB];
+  // ---- epilogue: this half's part of the item's partial slab ----
+  float* part = st.part + it.part_at;
+  float db0[4];
 #pragma unroll
-  for (int mb = 0; mb < WX_MB; ++mb) db0[mb] = row_sum(db0a[mb]);
+  for (int k = 0; k < 4; ++k) db0[k] = row_sum(db0a[k]);
 #pragma unroll
   for (int u = 0; u < 4 * WX_MAXCH; ++u) {
     const int j = 16 * u + i;
     if (u < 4 * nch && j < m) {
       const float mu = st.mu[bd.mk_off + j], sg = st.sigma[bd.mk_off + j];
 #pragma unroll
-      for (int mb = 0; mb < WX_MB; ++mb) {
-        const int c = 4 * mb + g;
-        if (c < w0) part[bd.woff[0] + c * m + j] = sg > 0.f ? (dW0a[u][mb] - mu * db0[mb]) / sg : 0.f;
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * (4 * h + k) + g;
+        if (c < w0) part[bd.woff[0] + c * m + j] = sg > 0.f ? (dW0a[u][k] - mu * db0[k]) / sg : 0.f;
       }
     }
   }
   if (i == 0) {
 #pragma unroll
-    for (int mb = 0; mb < WX_MB; ++mb)
-      if (4 * mb + g < w0) part[bd.boff[0] + 4 * mb + g] = db0[mb];
+    for (int k = 0; k < 4; ++k)
+      if (4 * (4 * h + k) + g < w0) part[bd.boff[0] + 4 * (4 * h + k) + g] = db0[k];
   }
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int c = 16 * cb + 4 * g + r, s = 16 * sb + i;
-        if (c < w0 && s < S) part[bd.woff[1] + s * w0 + c] = dW1a[cb][sb][r];
-      }
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
+  for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int s = 16 * nb + 4 * g + r;
-      const float v1 = row_sum(db1a[nb][r]), v2 = row_sum(dW2a[nb][r]);
-      if (i == 0 && s < S) {
-        part[bd.boff[1] + s] = v1;
-        part[bd.woff[2] + s] = v2;
-      }
+      const int c = 16 * h + 4 * g + r, s = 16 * sb + i;
+      if (c < w0 && s < S) part[bd.woff[1] + s * w0 + c] = dW1a[sb][r];
     }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int s = 16 * h + 4 * g + r;
+    const float v1 = row_sum(db1a[r]), v2 = row_sum(dW2a[r]);
+    if (i == 0 && s < S) {
+      part[bd.boff[1] + s] = v1;
+      part[bd.woff[2] + s] = v2;
+    }
+  }
   const double rs = wave_sum_d(rss);
-  if (lane == 0) st.rss_part[it.rss_at + slab] = rs;
+  if (h == 0 && lane == 0) st.rss_part[it.rss_at] = rs;
 }
 
 template <int BF>
