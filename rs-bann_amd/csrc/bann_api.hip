@@ -777,6 +777,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
         d.gx_b[l] = (int32_t)o;
         o += r4(d.widths[l]);
       }
+      d.gx_w0p = (int32_t)o;  // 3 x w0 x 64 nchunks bf16
+      o += r4((3ll * d.widths[0] * 64 * d.nchunks + 1) / 2);
       d.gx_dwo = (int32_t)o;
       o += 2 * ntile * r4(d.widths[h.L - 2]);
       d.gx_rss = (int32_t)o;

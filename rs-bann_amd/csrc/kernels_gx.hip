@@ -33,6 +33,8 @@
 // carry zero genotypes; their error is 0, so they add nothing to any gradient).
 // Gradients go to the branch's partial slabs part[split][P] (reduced in a fixed
 // order by k_update), the rss to rss_part: bitwise reproducible.
+#include <stdlib.h>
+
 #include "activations.h"
 #include "bann_internal.h"
 #include "kernel_util.h"
@@ -399,6 +401,259 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
 }
 
 // ---------------------------------------------------------------------------
+// the masked layer on the bf16 MFMA ("b3"): FWD0 (Z0 = G Wp_0^T) and GRAD0
+// (G^T delta0).  The genotype codes 0..2 are exact in bf16; the f32 operand x
+// is split into three bf16 planes hi + mid + lo (hi = bf16(x), mid =
+// bf16(x - hi), lo = bf16(x - hi - mid): 24 significant bits), so one 32-deep
+// K step is 3 v_mfma_f32_16x16x32_bf16 (48 cycles) where the f32 MFMA needs 8
+// (256 cycles): 5.3x the masked layer's rate, products exact, f32 accumulation
+// inside 64-deep K blocks and f64 across them as in k_gx_gemm.  The f32 path
+// stays selectable (BANN_GX_EXACT=1: exact f32 products).
+// LDS images [row][k] with 72-element rows (conflict-free 16-byte fragment reads).
+// ---------------------------------------------------------------------------
+#define GX_LDH 72  // bf16 row stride (elements)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mi, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r = x - (float)hi;  // exact
+  mi = (__bf16)r;
+  lo = (__bf16)(r - (float)mi);   // exact difference, rounded once
+}
+}  // namespace
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+namespace {
+// 16-lane-group transposing read (T10): lane 4q + p of a group gives the address of
+// row q, columns 4p .. 4p+3 of a 4 x 16 block; lane i receives column i, row q in
+// element q.  Two of them stacked = one 8-deep bf16 MFMA fragment along the rows.
+__device__ __forceinline__ bf16x8 tr16_pair(const __bf16* p0, const __bf16* p1) {
+  const v4s a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
+  const v4s b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p1));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+}  // namespace
+
+// LDS: the genotype chunk as G[marker][individual] (16 consecutive individuals per
+// thread: two 16-byte stores); FWD0 takes its A fragments (rows = individuals,
+// K = markers) from it by transposing reads and its B fragments from the W0 planes
+// [column][marker] (pre-split by k_gx_prep); GRAD0 takes A (rows = markers, K =
+// individuals) by row reads and B from the delta0 planes [individual][column]
+// (split on staging, 8-byte stores) by transposing reads.
+template <int PH>
+__global__ void __launch_bounds__(256, 4)
+    k_gx_gemm_b3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb,
+                 int total, int per) {
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[GX_T * GX_LDH];     // [marker][individual]
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3][GX_T * GX_LDH];  // FWD0 [column][marker], GRAD0 [individual][column]
+  const int q = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (q >= total) return;
+  int lo_ = 0, hi_ = nb;
+  while (hi_ - lo_ > 1) {
+    const int mid = (lo_ + hi_) >> 1;
+    if (prefix[mid] <= q) lo_ = mid;
+    else hi_ = mid;
+  }
+  const int b = blist[lo_];
+  const BranchDev& bd = st.br[b];
+  int tmc, tnc, ns;
+  gx_dims(st, bd, PH, 0, tmc, tnc, ns);
+  int r = q - prefix[lo_];
+  const int split = r / (tmc * tnc);
+  r -= split * tmc * tnc;
+  const int tm = r / tnc, tn = r % tnc;
+  const int64_t rows = gx_rows(st);
+  float* S = gx_base(st, bd);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int ar = 32 * (wv >> 1), bc = 32 * (wv & 1);
+  const uint8_t* img = st.xu2 + bd.x_off;
+  const int64_t tstride = (int64_t)bd.nchunks * 1024;
+  const int wo = bd.widths[0];
+  const int m64 = 64 * bd.nchunks;
+  int kb0 = 0, kb1;
+  if constexpr (PH == GX_FWD0) {
+    kb1 = bd.nchunks;
+  } else {
+    const int ntile = (st.nfrag + 3) / 4;
+    kb0 = (int)((int64_t)ntile * split / ns);
+    kb1 = (int)((int64_t)ntile * (split + 1) / ns);
+  }
+  const __bf16* W0p = reinterpret_cast<const __bf16*>(S + bd.gx_w0p);
+  const float* Dm = S + bd.gx_h[0];
+  const int64_t ldd = bd.gx_ld[0];
+  Blk rb;
+  v4i rw[6];
+  uint32_t rg = 0;
+  auto load = [&](int kb) {
+    if constexpr (PH == GX_FWD0) {
+      rg = geno_load(img + (int64_t)tm * tstride + (int64_t)kb * 1024);
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {  // 3 planes x 64 columns x 8 pieces of 8 markers
+        const int e = t + 256 * u, pl = e >> 9, row = (e >> 3) & 63, pc = e & 7;
+        const int col = 64 * tn + row;
+        rw[u] = col < wo ? *reinterpret_cast<const v4i*>(W0p + ((int64_t)pl * wo + col) * m64 + 64 * kb + 8 * pc)
+                         : v4i{0, 0, 0, 0};
+      }
+    } else {
+      rg = geno_load(img + (int64_t)kb * tstride + (int64_t)tm * 1024);
+      blk_load(rb, Dm, ldd, 64 * (int64_t)kb, rows, 64 * tn, wo);
+    }
+  };
+  double csp[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD0: column sums of delta0, columns 4 (t & 15) + x
+  auto store = [&]() {
+    int jl, dq;
+    geno_pos(jl, dq);
+    {
+      bf16x8 v0, v1;
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) {
+        v0[s2] = (__bf16)(float)((rg >> (2 * s2)) & 3u);
+        v1[s2] = (__bf16)(float)((rg >> (2 * s2 + 16)) & 3u);
+      }
+      *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq] = v0;
+      *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq + 8] = v1;
+    }
+    if constexpr (PH == GX_FWD0) {
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+        const int e = t + 256 * u, pl = e >> 9, row = (e >> 3) & 63, pc = e & 7;
+        *(v4i*)&Bs[pl][row * GX_LDH + 8 * pc] = rw[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // Bs[p][individual][column], four columns per store
+        const int e = t + 256 * u, rr = e >> 4, c4 = 4 * (e & 15);
+        bf16x4 h4, m4, l4;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          __bf16 hh, mm, ll;
+          split3(rb.v[u][x], hh, mm, ll);
+          h4[x] = hh;
+          m4[x] = mm;
+          l4[x] = ll;
+          csp[x] += (double)rb.v[u][x];
+        }
+        *(bf16x4*)&Bs[0][rr * GX_LDH + c4] = h4;
+        *(bf16x4*)&Bs[1][rr * GX_LDH + c4] = m4;
+        *(bf16x4*)&Bs[2][rr * GX_LDH + c4] = l4;
+      }
+    }
+  };
+
+  v4f acc[4];
+  double dacc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
+  }
+  const int tq = li >> 2, tp = li & 3;  // transposing reads: lane 4 tq + tp
+  if (kb0 < kb1) load(kb0);
+  for (int kb = kb0; kb < kb1; ++kb) {
+    store();
+    __syncthreads();
+    if (kb + 1 < kb1) load(kb + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ko = 32 * ks + 8 * lq;  // this lane group's 8 K slots
+      bf16x8 a0, a1;
+      if constexpr (PH == GX_FWD0) {  // rows = individuals, K = markers: transposed from Gs
+        a0 = tr16_pair(&Gs[(ko + tq) * GX_LDH + ar + 4 * tp], &Gs[(ko + 4 + tq) * GX_LDH + ar + 4 * tp]);
+        a1 = tr16_pair(&Gs[(ko + tq) * GX_LDH + ar + 16 + 4 * tp], &Gs[(ko + 4 + tq) * GX_LDH + ar + 16 + 4 * tp]);
+      } else {  // rows = markers, K = individuals: row reads
+        a0 = *(const bf16x8*)&Gs[(ar + li) * GX_LDH + ko];
+        a1 = *(const bf16x8*)&Gs[(ar + 16 + li) * GX_LDH + ko];
+      }
+#pragma unroll
+      for (int pl = 2; pl >= 0; --pl) {  // small planes first
+        bf16x8 b0, b1;
+        if constexpr (PH == GX_FWD0) {  // B[k = marker][n = column] from Bs[column][marker]
+          b0 = *(const bf16x8*)&Bs[pl][(bc + li) * GX_LDH + ko];
+          b1 = *(const bf16x8*)&Bs[pl][(bc + 16 + li) * GX_LDH + ko];
+        } else {  // B[k = individual][n = column] transposed from Bs[individual][column]
+          b0 = tr16_pair(&Bs[pl][(ko + tq) * GX_LDH + bc + 4 * tp], &Bs[pl][(ko + 4 + tq) * GX_LDH + bc + 4 * tp]);
+          b1 = tr16_pair(&Bs[pl][(ko + tq) * GX_LDH + bc + 16 + 4 * tp],
+                         &Bs[pl][(ko + 4 + tq) * GX_LDH + bc + 16 + 4 * tp]);
+        }
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[3], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      dacc[x][0] += (double)acc[x].x;
+      dacc[x][1] += (double)acc[x].y;
+      dacc[x][2] += (double)acc[x].z;
+      dacc[x][3] += (double)acc[x].w;
+      acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // every wave is done with the stage before it is refilled
+  }
+
+  if constexpr (PH == GX_FWD0) {
+    const float* bias = S + bd.gx_b[0];
+    float* Ao = S + bd.gx_a[0];
+    float* Ho = S + bd.gx_h[0];
+    const int64_t ld = bd.gx_ld[0];
+    const int act = bd.act;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+      const float bj = bias[j];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        const float z = (float)dacc[x][y] + bj;
+        const float a = act_h(z, act);
+        Ao[row * ld + j] = a;
+        Ho[row * ld + j] = act_dh(z, a, act);
+      }
+    }
+  } else {
+    // column sums: 16 threads per column group, added in thread order (deterministic)
+    double* cs_s = reinterpret_cast<double*>(&Bs[0][0]);  // [16][64], the staging is free now
+#pragma unroll
+    for (int x = 0; x < 4; ++x) cs_s[(t >> 4) * 64 + 4 * (t & 15) + x] = csp[x];
+    __syncthreads();
+    double* cs_f = reinterpret_cast<double*>(&Gs[0]);  // [64]
+    if (t < GX_T) {
+      double c = 0.0;
+      for (int k = 0; k < 16; ++k) c += cs_s[k * 64 + t];
+      cs_f[t] = c;
+    }
+    __syncthreads();
+    float* part = st.part + bd.part_off + (int64_t)split * bd.P;
+    const int wi = bd.m, win = bd.m;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int jc = bc + 16 * (x & 1) + li;
+      const int j = 64 * tn + jc;
+      if (j >= wo) continue;
+      const double cs = cs_f[jc];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        if (i >= wi) continue;
+        const float sg = st.sigma[bd.mk_off + i];
+        const double v = sg > 0.f ? (dacc[x][y] - (double)st.mu[bd.mk_off + i] * cs) / (double)sg : 0.0;
+        part[bd.woff[0] + (int64_t)j * win + i] = (float)v;
+      }
+    }
+    if (tm == 0 && t < GX_T && 64 * tn + t < wo) part[bd.boff[0] + 64 * tn + t] = (float)cs_f[t];  // db0
+  }
+}
+
+// ---------------------------------------------------------------------------
 // PREP: padded weights, W0 / sigma, c0 = b0 - mu^T (W0 / sigma) (f64), biases
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __restrict__ blist) {
@@ -424,6 +679,20 @@ __global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __r
     }
   }
   __syncthreads();
+  {  // W0 / sigma as three bf16 planes [3][w0][64 nchunks], zero padded (k_gx_gemm_b3)
+    const int w0 = bd.widths[0], m64 = 64 * bd.nchunks, ld = bd.gx_wld[0];
+    const float* Wp = S + bd.gx_w[0];
+    __bf16* P3 = reinterpret_cast<__bf16*>(S + bd.gx_w0p);
+    const int64_t tot = (int64_t)w0 * m64;
+    for (int64_t e = threadIdx.x; e < tot; e += 256) {
+      const int k = (int)(e / m64), j = (int)(e - (int64_t)k * m64);
+      __bf16 hh = (__bf16)0.f, mm = (__bf16)0.f, ll = (__bf16)0.f;
+      if (j < bd.m) split3(Wp[(int64_t)k * ld + j], hh, mm, ll);
+      P3[e] = hh;
+      P3[tot + e] = mm;
+      P3[2 * tot + e] = ll;
+    }
+  }
   // c0 (one thread per unit, f64 in marker order) and the other biases
   {
     const int m = bd.m, ld = bd.gx_wld[0];
@@ -534,6 +803,16 @@ void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, con
   if (nb <= 0 || total <= 0) return;
   const int per = (total + 7) / 8;
   const dim3 g(8 * per), blk(256);
+  const char* ex = getenv("BANN_GX_EXACT");  // 1: the masked layer on the exact-f32 MFMA path
+  const bool exact = ex && atoi(ex) != 0;
+  if (!exact && ph == GX_FWD0) {
+    hipLaunchKernelGGL(k_gx_gemm_b3<GX_FWD0>, g, blk, 0, s, st, blist, prefix, nb, total, per);
+    return;
+  }
+  if (!exact && ph == GX_GRAD0) {
+    hipLaunchKernelGGL(k_gx_gemm_b3<GX_GRAD0>, g, blk, 0, s, st, blist, prefix, nb, total, per);
+    return;
+  }
   switch (ph) {
     case GX_FWD0: hipLaunchKernelGGL(k_gx_gemm<GX_FWD0>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;
     case GX_FWD: hipLaunchKernelGGL(k_gx_gemm<GX_FWD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;

@@ -608,6 +608,38 @@ def test_default_arch_full_n(Ctx):
     ctx.close()
 
 
+@pytest.mark.parametrize("exact", ["0", "1"])
+def test_layered_masked_layer_modes(Ctx, exact):
+    """gx's masked layer on the bf16 MFMA (genotype codes exact, the f32 operand as
+    three bf16 planes; default) and on the f32 MFMA (BANN_GX_EXACT=1): both within
+    the 1e-5 tolerance on a default-architecture branch with several row splits."""
+    cfg = dict(n=9000, m=300, widths=[150, 150, 1], act="tanh", prior="ridge_ard")
+    rng, g, snps, br = make_problem(cfg, 47)
+    os.environ["BANN_GX_EXACT"] = exact
+    try:
+        ctx = build_context(Ctx, g, [dict(snps=snps, branch=br, y=np.zeros(cfg["n"]))])
+        X = oracle_inputs(ctx, g, snps)
+        f = O.predict(br, X)
+        y = (f + rng.normal(scale=max(float(np.std(f)), 0.1), size=cfg["n"])).astype(np.float32).astype(np.float64)
+        ctx.set_target(0, y)
+        grad, rss = ctx.log_density_gradient(0)
+        pred = ctx.predict(0)
+    finally:
+        del os.environ["BANN_GX_EXACT"]
+    from test_oracle_kats import cancellation_tol
+    ogw, ogb, orss = O.log_density_gradient(br, X, y)
+    gw, gb = layer_views(br, grad)
+    for l in range(br.num_layers):
+        assert norm_rel(gw[l], ogw[l]) < TOL, ("W", l, norm_rel(gw[l], ogw[l]))
+    # bias gradients: sums over 9000 rows of f32 deltas with heavy cancellation; the
+    # exact-f32 path lands at 0.5-2e-5 here too (tools/gx_prec.py), so the f32
+    # rounding bound of that sum is the tolerance, as for the KAT bias gradients
+    for l in range(br.num_layers - 1):
+        assert norm_rel(gb[l], ogb[l]) < cancellation_tol(br, X, l, y), ("b", l, norm_rel(gb[l], ogb[l]))
+    assert scalar_close(rss, orss) and norm_rel(pred, f) < TOL
+    ctx.close()
+
+
 def test_layered_scratch_groups_and_packing(Ctx):
     """gx branches of mixed shapes in several scratch groups (a 1 MiB budget puts
     every branch in its own group, so later groups overwrite the scratch of
