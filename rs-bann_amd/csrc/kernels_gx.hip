@@ -79,29 +79,45 @@ __device__ __forceinline__ void gx_dims(const DevState& st, const BranchDev& bd,
 // a 64 x 64 block of a row-major f32 matrix M[r][c] (row stride ld, a multiple of
 // 4): element (r, c) of the block = M[r0 + r][c0 + c] when r0 + r < rmax and
 // c0 + c < cmax, else 0.  Thread t holds rows (t + 256 u) >> 4, columns 4 (t & 15).
+// The loads are only issued here; the edge masking waits until blk_fix, after the
+// K block's MFMAs (masking right after the load would make the compiler wait for
+// the data there and expose the full memory latency every block).  blk_fix
+// recomputes the bounds instead of keeping them in registers.
 struct Blk {
   v4f v[4];
 };
-__device__ __forceinline__ void blk_load(Blk& s, const float* __restrict__ M, int64_t ld, int64_t r0, int64_t rmax,
-                                         int c0, int cmax) {
+struct BlkBounds {
+  int64_t r0, rmax;
+  int c0, cmax;
+};
+__device__ __forceinline__ int blk_nv(const BlkBounds& k, int u) {
+  const int e = threadIdx.x + 256 * u;
+  const int64_t r = k.r0 + (e >> 4);
+  const int c = k.c0 + 4 * (e & 15);
+  return r < k.rmax ? min(max(k.cmax - c, 0), 4) : 0;
+}
+__device__ __forceinline__ void blk_load(Blk& s, const float* __restrict__ M, int64_t ld, const BlkBounds& k) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = t + 256 * u;
-    const int64_t r = r0 + (e >> 4);
-    const int c = c0 + 4 * (e & 15);
     v4f x = {0.f, 0.f, 0.f, 0.f};
-    if (r < rmax && c < cmax) {
-      x = *(const v4f*)(M + r * ld + c);
-      if (c + 1 >= cmax) x.y = 0.f;
-      if (c + 2 >= cmax) x.z = 0.f;
-      if (c + 3 >= cmax) x.w = 0.f;
-    }
+    if (blk_nv(k, u) > 0) x = *(const v4f*)(M + (k.r0 + (e >> 4)) * ld + k.c0 + 4 * (e & 15));  // rows padded to 4
     s.v[u] = x;
   }
 }
+__device__ __forceinline__ void blk_fix(Blk& s, const BlkBounds& k) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int nv = blk_nv(k, u);
+    if (nv < 2) s.v[u].y = 0.f;
+    if (nv < 3) s.v[u].z = 0.f;
+    if (nv < 4) s.v[u].w = 0.f;
+  }
+}
 // LDS [r][c] (the block's rows are the MFMA rows, its columns the K index)
-__device__ __forceinline__ void blk_store(const Blk& s, float* L) {
+__device__ __forceinline__ void blk_store(Blk& s, const BlkBounds& k, float* L) {
+  blk_fix(s, k);
   const int t = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -110,7 +126,8 @@ __device__ __forceinline__ void blk_store(const Blk& s, float* L) {
   }
 }
 // LDS [c][r] (the block's columns are the MFMA rows, its rows the K index)
-__device__ __forceinline__ void blk_store_t(const Blk& s, float* L) {
+__device__ __forceinline__ void blk_store_t(Blk& s, const BlkBounds& k, float* L) {
+  blk_fix(s, k);
   const int t = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -160,8 +177,9 @@ __device__ __forceinline__ void geno_store_mi(uint32_t g, float* L) {
 // ---------------------------------------------------------------------------
 // the GEMM phases
 // ---------------------------------------------------------------------------
+// GRAD (two staged operands + f64 accumulators) at 3 workgroups per CU: 4 would spill
 template <int PH>
-__global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
+__global__ void __launch_bounds__(256, GX_NBUF == 1 ? (PH == GX_GRAD ? 3 : 4) : 2)
     k_gx_gemm(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
               int total, int per) {
   __shared__ float As[GX_NBUF][GX_LDS];
@@ -246,40 +264,38 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
   // stage K block kb into registers
   Blk ra, rb;
   uint32_t rg = 0;
-  auto load = [&](int kb) {
-    if constexpr (PH == GX_FWD0) {
-      rg = geno_load(img + (int64_t)tm * tstride + (int64_t)kb * 1024);
-      blk_load(rb, Bm, ldb, 64 * tn, wo, 64 * kb, (int)kcount);
-    } else if constexpr (PH == GX_FWD) {
-      blk_load(ra, Am, lda, 64 * (int64_t)tm, rows, 64 * kb, (int)kcount);
-      blk_load(rb, Bm, ldb, 64 * tn, wo, 64 * kb, (int)kcount);
-    } else if constexpr (PH == GX_BWD) {
-      blk_load(ra, Am, lda, 64 * (int64_t)tm, rows, 64 * kb, (int)kcount);
-      blk_load(rb, Bm, ldb, 64 * kb, (int)kcount, 64 * tn, wo);
-    } else if constexpr (PH == GX_GRAD) {
-      blk_load(ra, Am, lda, 64 * (int64_t)kb, rows, 64 * tm, wi);
-      blk_load(rb, Bm, ldb, 64 * (int64_t)kb, rows, 64 * tn, wo);
-    } else {
-      rg = geno_load(img + (int64_t)kb * tstride + (int64_t)tm * 1024);
-      blk_load(rb, Bm, ldb, 64 * (int64_t)kb, rows, 64 * tn, wo);
-    }
+  // the operand blocks of K block kb
+  auto bnd_a = [&](int kb) -> BlkBounds {
+    if constexpr (PH == GX_GRAD) return BlkBounds{64 * (int64_t)kb, rows, 64 * tm, wi};
+    return BlkBounds{64 * (int64_t)tm, rows, 64 * kb, (int)kcount};
   };
-  auto store = [&](int buf) {
+  auto bnd_b = [&](int kb) -> BlkBounds {
+    if constexpr (PH == GX_FWD0 || PH == GX_FWD) return BlkBounds{64 * (int64_t)tn, wo, 64 * kb, (int)kcount};
+    if constexpr (PH == GX_BWD) return BlkBounds{64 * (int64_t)kb, kcount, 64 * tn, wo};
+    return BlkBounds{64 * (int64_t)kb, rows, 64 * tn, wo};
+  };
+  auto load = [&](int kb) {
+    if constexpr (PH == GX_FWD0) rg = geno_load(img + (int64_t)tm * tstride + (int64_t)kb * 1024);
+    if constexpr (PH == GX_GRAD0) rg = geno_load(img + (int64_t)kb * tstride + (int64_t)tm * 1024);
+    if constexpr (PH == GX_FWD || PH == GX_BWD || PH == GX_GRAD) blk_load(ra, Am, lda, bnd_a(kb));
+    blk_load(rb, Bm, ldb, bnd_b(kb));
+  };
+  auto store = [&](int buf, int kb) {
     if constexpr (PH == GX_FWD0) {
       geno_store_im(rg, As[buf]);
-      blk_store(rb, Bs[buf]);
+      blk_store(rb, bnd_b(kb), Bs[buf]);
     } else if constexpr (PH == GX_FWD) {
-      blk_store(ra, As[buf]);
-      blk_store(rb, Bs[buf]);
+      blk_store(ra, bnd_a(kb), As[buf]);
+      blk_store(rb, bnd_b(kb), Bs[buf]);
     } else if constexpr (PH == GX_BWD) {
-      blk_store(ra, As[buf]);
-      blk_store_t(rb, Bs[buf]);
+      blk_store(ra, bnd_a(kb), As[buf]);
+      blk_store_t(rb, bnd_b(kb), Bs[buf]);
     } else if constexpr (PH == GX_GRAD) {
-      blk_store_t(ra, As[buf]);
-      blk_store_t(rb, Bs[buf]);
+      blk_store_t(ra, bnd_a(kb), As[buf]);
+      blk_store_t(rb, bnd_b(kb), Bs[buf]);
     } else {
       geno_store_mi(rg, As[buf]);
-      blk_store_t(rb, Bs[buf]);
+      blk_store_t(rb, bnd_b(kb), Bs[buf]);
     }
   };
 
@@ -297,7 +313,7 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
   double cs = 0.0;  // want_cs: column sum of the B block (delta) over the K range, thread t < 64 = column t
   if (kb0 < kb1) {
     load(kb0);
-    store(0);
+    store(0, kb0);
   }
   __syncthreads();
   for (int kb = kb0; kb < kb1; ++kb) {
@@ -333,7 +349,7 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? 4 : 2)
       }
     }
     if (GX_NBUF == 1) __syncthreads();  // every wave is done with the stage before it is refilled
-    if (kb + 1 < kb1) store(GX_NBUF == 1 ? 0 : buf ^ 1);
+    if (kb + 1 < kb1) store(GX_NBUF == 1 ? 0 : buf ^ 1, kb + 1);
     __syncthreads();
   }
 
@@ -446,7 +462,7 @@ __device__ __forceinline__ bf16x8 tr16_pair(const __bf16* p0, const __bf16* p1) 
 // individuals) by row reads and B from the delta0 planes [individual][column]
 // (split on staging, 8-byte stores) by transposing reads.
 template <int PH>
-__global__ void __launch_bounds__(256, 4)
+__global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
     k_gx_gemm_b3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb,
                  int total, int per) {
   __shared__ __attribute__((aligned(16))) __bf16 Gs[GX_T * GX_LDH];     // [marker][individual]
@@ -497,16 +513,17 @@ __global__ void __launch_bounds__(256, 4)
       for (int u = 0; u < 6; ++u) {  // 3 planes x 64 columns x 8 pieces of 8 markers
         const int e = t + 256 * u, pl = e >> 9, row = (e >> 3) & 63, pc = e & 7;
         const int col = 64 * tn + row;
-        rw[u] = col < wo ? *reinterpret_cast<const v4i*>(W0p + ((int64_t)pl * wo + col) * m64 + 64 * kb + 8 * pc)
-                         : v4i{0, 0, 0, 0};
+        v4i v = v4i{0, 0, 0, 0};
+        if (col < wo) v = *reinterpret_cast<const v4i*>(W0p + ((int64_t)pl * wo + col) * m64 + 64 * kb + 8 * pc);
+        rw[u] = v;
       }
     } else {
       rg = geno_load(img + (int64_t)kb * tstride + (int64_t)tm * 1024);
-      blk_load(rb, Dm, ldd, 64 * (int64_t)kb, rows, 64 * tn, wo);
+      blk_load(rb, Dm, ldd, BlkBounds{64 * (int64_t)kb, rows, 64 * tn, wo});
     }
   };
   double csp[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD0: column sums of delta0, columns 4 (t & 15) + x
-  auto store = [&]() {
+  auto store = [&](int kb) {
     int jl, dq;
     geno_pos(jl, dq);
     {
@@ -526,6 +543,7 @@ __global__ void __launch_bounds__(256, 4)
         *(v4i*)&Bs[pl][row * GX_LDH + 8 * pc] = rw[u];
       }
     } else {
+      blk_fix(rb, BlkBounds{64 * (int64_t)kb, rows, 64 * tn, wo});
 #pragma unroll
       for (int u = 0; u < 4; ++u) {  // Bs[p][individual][column], four columns per store
         const int e = t + 256 * u, rr = e >> 4, c4 = 4 * (e & 15);
@@ -557,7 +575,7 @@ __global__ void __launch_bounds__(256, 4)
   const int tq = li >> 2, tp = li & 3;  // transposing reads: lane 4 tq + tp
   if (kb0 < kb1) load(kb0);
   for (int kb = kb0; kb < kb1; ++kb) {
-    store();
+    store(kb);
     __syncthreads();
     if (kb + 1 < kb1) load(kb + 1);
 #pragma unroll
