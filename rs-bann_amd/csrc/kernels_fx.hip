@@ -69,6 +69,10 @@ __device__ __forceinline__ void vm_wait(int k) {
   }
 }
 
+__device__ __forceinline__ float sgpr_f(float v) {  // a wave-uniform value, pinned to a scalar register
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+
 __device__ __forceinline__ float comb4(v4i d) {  // sum_d D_d 2^(-7 d)
   return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
 }
@@ -196,6 +200,22 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+#if !(BANN_ABLATE & 262144)
+  // head weights as wave-uniform values: scalar registers for the whole item (the
+  // per-tile LDS broadcasts serialised the head on their latencies)
+  float uW[NL][4][4], uB[NH][4];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        uW[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l][4 * j + k]) : 0.f;
+    if (l < NH)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l][16 + k]);
+  }
+#endif
 
   // ---- per-lane LDS offsets ----
   const int gsw = g & 1;
@@ -219,6 +239,12 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   auto issue_chunk = [&](int tt, int sl, int c) {
 #if BANN_ABLATE & 8
     return;  // profiling build: no genotype / target traffic
+#endif
+#if BANN_ABLATE & 131072
+    // profiling build: every DMA reads branch 0's first two tiles (L2-resident)
+    glds16(reinterpret_cast<const char*>(st.xu2) + lane * 16 + (int64_t)(tt & 1) * tile_bytes + c * 1024,
+           &s_x[wave][sl][c * 1024]);
+    return;
 #endif
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
@@ -264,6 +290,9 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime(), ntl = 0;
 #endif
   int tt = tb + wave, sl = 0;
+#if BANN_ABLATE & 16
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+#endif
   if (tt < te) {
     for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
@@ -381,6 +410,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     if (false)
 #endif
     {
+#if BANN_ABLATE & 262144
       float Wh[NL][4][4], Bh[NH][4];
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
@@ -398,6 +428,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
         }
       }
+#else
+      const auto& Wh = uW;
+      const auto& Bh = uB;
+#endif
       float z[NH][4], a[NH][4];
       z[0][0] = z0 + Bh[0][0];
       z[0][1] = z1 + Bh[0][1];
@@ -456,6 +490,12 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 
     __builtin_amdgcn_sched_barrier(0);
     FX_STAMP(3);
+    // the backward's first genotype windows: their LDS reads fly under the digit phase
+    constexpr int PD = 8;
+    uint32_t wq[PD];
+#pragma unroll
+    for (int u = 0; u < PD; ++u)
+      wq[u] = (NCH != 0 || u < 4 * nch) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
     // ---- delta0 -> signed digits at the running per-column scale 2^(R - 132) ----
     // running scale check: a column needs a (new) scale only when some lane's
     // |delta| reaches 2^(R - 126) (or R is unset); then the exact wave max of
@@ -463,13 +503,13 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     int dl[4] = {0, 0, 0, 0};
     bool grow = false;
     {
-      bool need = false;
+      bool lane_need = false;  // one ballot for the four columns (no compare -> branch chain)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ek = (int)((fbits(d[k]) >> 23) & 0xFFu);
-        need = need || __builtin_amdgcn_ballot_w64(ek > (R[k] ? R[k] : 5)) != 0;
+        lane_need |= ek > (R[k] ? R[k] : 5);
       }
-      if (need) {
+      if (__builtin_amdgcn_ballot_w64(lane_need) != 0) {
         const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
         const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
         const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
@@ -509,11 +549,6 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
-      constexpr int PD = 8;
-      uint32_t wq[PD];
-#pragma unroll
-      for (int u = 0; u < PD; ++u)
-        wq[u] = (NCH != 0 || u < 4 * nch) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
       // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
       auto unpack = [](uint32_t wv) -> v4i {
 #if BANN_ABLATE & 8192
@@ -579,8 +614,11 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   }
 #endif
 #if BANN_ABLATE & 16
+  // p6 / p7: the loop's 100 MHz real time and shader cycles (their ratio: the clock)
+  ph[6] = __builtin_amdgcn_s_memrealtime() - rt0;
+  ph[7] = __builtin_amdgcn_s_memtime() - mt0;
   if (lane == 0 && st.dbg) {
-    for (int i = 0; i < 6; ++i) atomicAdd(&st.dbg[i], ph[i]);
+    for (int i = 0; i < 8; ++i) atomicAdd(&st.dbg[i], ph[i]);
     atomicAdd(&st.dbg[15], ntl);
   }
 #endif
@@ -791,6 +829,20 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+#if !(BANN_ABLATE & 262144)
+  float uW[NL][4][4], uB[NH][4];  // head weights in scalar registers (as fx)
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        uW[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l * 20 + 4 * j + k]) : 0.f;
+    if (l < NH)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l * 20 + 16 + k]);
+  }
+#endif
 
   const int gsw = g & 1;
   const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
@@ -924,6 +976,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     if (more) issue_y(tt + 1, sl ^ 1);
     float d[4];
     {
+#if BANN_ABLATE & 262144
       float Wh[NL][4][4], Bh[NH][4];
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
@@ -941,6 +994,10 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
           for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
         }
       }
+#else
+      const auto& Wh = uW;
+      const auto& Bh = uB;
+#endif
       float z[NH][4], a[NH][4];
       z[0][0] = z0 + Bh[0][0];
       z[0][1] = z1 + Bh[0][1];
@@ -1001,13 +1058,13 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     int dl[4] = {0, 0, 0, 0};
     bool grow = false;
     {
-      bool need = false;
+      bool lane_need = false;  // one ballot for the four columns (no compare -> branch chain)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ek = (int)((fbits(d[k]) >> 23) & 0xFFu);
-        need = need || __builtin_amdgcn_ballot_w64(ek > (R[k] ? R[k] : 5)) != 0;
+        lane_need |= ek > (R[k] ? R[k] : 5);
       }
-      if (need) {
+      if (__builtin_amdgcn_ballot_w64(lane_need) != 0) {
         const uint32_t e01 = wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
         const uint32_t e23 = wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
         const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
