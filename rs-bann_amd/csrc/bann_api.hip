@@ -779,6 +779,10 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
       }
       d.gx_w0p = (int32_t)o;  // 3 x w0 x 64 nchunks bf16
       o += r4((3ll * d.widths[0] * 64 * d.nchunks + 1) / 2);
+      for (int l = 1; l < h.L - 1; ++l) {  // 3 x w_l x r32(win_l) bf16
+        d.gx_wp[l] = (int32_t)o;
+        o += r4((3ll * d.widths[l] * ((d.win[l] + 31) & ~31) + 1) / 2);
+      }
       d.gx_dwo = (int32_t)o;
       o += 2 * ntile * r4(d.widths[h.L - 2]);
       d.gx_rss = (int32_t)o;

@@ -49,6 +49,7 @@ struct BranchDev {
   int32_t gx_dwo;             // head: f64 dW_out partials [tile][S]
   int32_t gx_rss;             // head: f64 rss partials [tile]
   int32_t gx_w0p;             // W0 / sigma as three bf16 planes [3][w0][64 nchunks] (masked layer on bf16 MFMA)
+  int32_t gx_wp[BANN_MAXL];   // Wp_l, 1 <= l < L-1, as three bf16 planes [3][w_l][win_l rounded up to 32] (hidden GEMMs)
   // precision coordinates (precision_vec order, params.rs:272-289) for joint HMC
   int64_t q_off;              // offset into the per-precision arrays (phi, ...)
   int32_t nq;                 // num precisions

@@ -35,11 +35,14 @@
 // order by k_update), the rss to rss_part: bitwise reproducible.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "activations.h"
 #include "bann_internal.h"
 #include "kernel_util.h"
 
 #define GX_T 64                // output tile edge, K block depth
+#define GX_PREP_Y 16           // k_gx_prep workgroups per branch
 #define GX_LD 68               // LDS row stride (floats)
 #define GX_LDS (GX_T * GX_LD)  // floats per operand block
 #ifndef GX_NBUF
@@ -173,6 +176,85 @@ __device__ __forceinline__ void geno_store_mi(uint32_t g, float* L) {
 }
 
 }  // namespace
+
+// the epilogue of a 64 x 64 output tile: lane holds rows ar + 16 X + 4 lq + y and
+// columns bc + 16 Y + li of accumulator x = 2 X + Y (f32 acc, or the f64 dacc when
+// F64).  FWD0 / FWD: A = h(Z + b), H = h'(Z + b); BWD: delta_{l-1} = H * acc in
+// place; GRAD / GRAD0: the weight gradient into the split's partial slab (GRAD0
+// with the standardisation, column sums cs_col of delta0 in LDS) and, in the
+// tm == 0 tiles, db from the column sum cs of thread t < 64.
+template <int PH, bool F64>
+__device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev& bd, float* S, int l, int tm, int tn,
+                                            int split, int wi, int wo, int ar, int bc, int li, int lq, const v4f (&acc)[4],
+                                            const double (&dacc)[4][4], double cs, const double* cs_col) {
+  const int t = threadIdx.x;
+  if constexpr (PH == GX_FWD0 || PH == GX_FWD) {
+    const int lay = PH == GX_FWD0 ? 0 : l;
+    const float* bias = S + bd.gx_b[lay];
+    float* Ao = S + bd.gx_a[lay];
+    float* Ho = S + bd.gx_h[lay];
+    const int64_t ld = bd.gx_ld[lay];
+    // the activation as a compile-time kind (activations.h)
+    auto out = [&](auto kind) {
+      constexpr int ACT = decltype(kind)::value;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const int j = 64 * tn + bc + 16 * (x & 1) + li;
+        if (j >= wo) continue;
+        const float bj = bias[j];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+          const float z = (F64 ? (float)dacc[x][y] : acc[x][y]) + bj;  // mid_layer_pre_activation: matmul + bias
+          const float a = ACT == 0 ? fast_tanh(z) : act_h_t<ACT>(z);  // tanh to ~2 ulp (layer outputs feed GEMMs)
+          Ao[row * ld + j] = a;
+          Ho[row * ld + j] = act_dh_t<ACT>(z, a);
+        }
+      }
+    };
+    switch (bd.act) {
+      case 0: out(std::integral_constant<int, 0>{}); break;
+      case 1: out(std::integral_constant<int, 1>{}); break;
+      case 2: out(std::integral_constant<int, 2>{}); break;
+      case 3: out(std::integral_constant<int, 3>{}); break;
+      default: out(std::integral_constant<int, 4>{}); break;
+    }
+  } else if constexpr (PH == GX_BWD) {
+    float* Hd = S + bd.gx_h[l - 1];
+    const int64_t ld = bd.gx_ld[l - 1];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        Hd[row * ld + j] *= acc[x][y];  // delta = h'(z) * (delta_next W^T)
+      }
+    }
+  } else {
+    float* part = st.part + bd.part_off + (int64_t)split * bd.P;
+    const int lay = PH == GX_GRAD ? l : 0;
+    const int win = bd.win[lay];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      if (j >= wo) continue;
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        if (i >= wi) continue;
+        double v = dacc[x][y];
+        if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
+          const float sg = st.sigma[bd.mk_off + i];
+          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_col[bc + 16 * (x & 1) + li]) / (double)sg : 0.0;
+        }
+        part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
+      }
+    }
+    if (tm == 0 && t < GX_T && 64 * tn + t < wo) part[bd.boff[lay] + 64 * tn + t] = (float)cs;  // db_l
+  }
+}
 
 // ---------------------------------------------------------------------------
 // the GEMM phases
@@ -353,67 +435,11 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? (PH == GX_GRAD ? 3 : 4) : 
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds rows ar + 16 X + 4 lq + y, columns bc + 16 Y + li (acc x = 2 X + Y)
-  if constexpr (PH == GX_FWD0 || PH == GX_FWD) {
-    const int lay = PH == GX_FWD0 ? 0 : l;
-    const float* bias = S + bd.gx_b[lay];
-    float* Ao = S + bd.gx_a[lay];
-    float* Ho = S + bd.gx_h[lay];
-    const int64_t ld = bd.gx_ld[lay];
-    const int act = bd.act;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
-      if (j >= wo) continue;
-      const float bj = bias[j];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
-        const float z = (F64 ? (float)dacc[x][y] : acc[x][y]) + bj;  // mid_layer_pre_activation: matmul + bias
-        const float a = act_h(z, act);
-        Ao[row * ld + j] = a;
-        Ho[row * ld + j] = act_dh(z, a, act);
-      }
-    }
-  } else if constexpr (PH == GX_BWD) {
-    float* Hd = S + bd.gx_h[l - 1];
-    const int64_t ld = bd.gx_ld[l - 1];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
-      if (j >= wo) continue;
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
-        Hd[row * ld + j] *= acc[x][y];  // delta = h'(z) * (delta_next W^T)
-      }
-    }
-  } else {
-    float* part = st.part + bd.part_off + (int64_t)split * bd.P;
-    const int lay = PH == GX_GRAD ? l : 0;
-    const int win = bd.win[lay];
-    if (PH == GX_GRAD0) {
-      if (t < GX_T) cs_s[t] = cs;
-      __syncthreads();
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
-      if (j >= wo) continue;
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
-        if (i >= wi) continue;
-        double v = dacc[x][y];
-        if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
-          const float sg = st.sigma[bd.mk_off + i];
-          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_s[bc + 16 * (x & 1) + li]) / (double)sg : 0.0;
-        }
-        part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
-      }
-    }
-    if (tm == 0 && t < GX_T && 64 * tn + t < wo) part[bd.boff[lay] + 64 * tn + t] = (float)cs;  // db_l
+  if constexpr (PH == GX_GRAD0) {
+    if (t < GX_T) cs_s[t] = cs;
+    __syncthreads();
   }
+  gx_epilogue<PH, F64>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, cs_s);
 }
 
 // ---------------------------------------------------------------------------
@@ -618,25 +644,7 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
   }
 
   if constexpr (PH == GX_FWD0) {
-    const float* bias = S + bd.gx_b[0];
-    float* Ao = S + bd.gx_a[0];
-    float* Ho = S + bd.gx_h[0];
-    const int64_t ld = bd.gx_ld[0];
-    const int act = bd.act;
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
-      if (j >= wo) continue;
-      const float bj = bias[j];
-#pragma unroll
-      for (int y = 0; y < 4; ++y) {
-        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
-        const float z = (float)dacc[x][y] + bj;
-        const float a = act_h(z, act);
-        Ao[row * ld + j] = a;
-        Ho[row * ld + j] = act_dh(z, a, act);
-      }
-    }
+    gx_epilogue<GX_FWD0, true>(st, bd, S, 0, tm, tn, split, 0, wo, ar, bc, li, lq, acc, dacc, 0.0, nullptr);
   } else {
     // column sums: 16 threads per column group, added in thread order (deterministic)
     double* cs_s = reinterpret_cast<double*>(&Bs[0][0]);  // [16][64], the staging is free now
@@ -672,57 +680,344 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
 }
 
 // ---------------------------------------------------------------------------
+// the hidden-layer GEMMs on the bf16 MFMA ("x3"): FWD l, BWD l and GRAD l with
+// BOTH f32 operands split into three bf16 planes (x = x0 + x1 + x2, 24
+// significant bits, split3) and the six plane products of weight >= 2^-16:
+//   a b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0) + O(2^-24 |a b|),
+// every product keeps f32's accuracy; a 32-deep K step is six
+// v_mfma_f32_16x16x32_bf16 (96 cycles) where the f32 MFMA takes eight 16x16x4
+// (256 cycles).  K blocks of 32: the 3 + 3 planes of a stage take 30 KiB, four
+// workgroups per CU.  An operand whose MFMA rows are contiguous in memory (FWD:
+// A_{l-1} and Wp_l; BWD: delta_l) is staged [row][k] and read as 16-byte
+// fragments; the others (BWD: Wp_l read transposed; GRAD: A_{l-1} and delta_l,
+// K = individuals) are staged [k][row] and read with ds_read_b64_tr_b16.  f32
+// accumulation inside a K block, f64 across blocks where K is long (GRAD: the
+// rows).  BANN_GX_EXACT=1 keeps k_gx_gemm (f32 MFMA) for every phase.
+// ---------------------------------------------------------------------------
+#define GX_KB 32    // K block depth
+#define GX_RK 40    // [row][k] stride (bf16 elements): 80-byte rows, conflict-free 16-byte reads
+#define GX_KR 72    // [k][row] stride (bf16 elements), as GX_LDH
+#define GX_PL 2560  // elements per plane: max(64 x GX_RK, GX_KB x GX_KR)
+
+namespace {
+// a 64 (MFMA rows) x 32 (K) block of an f32 matrix, 2 x 4 consecutive elements per
+// thread.  RK: M[r][k], thread e = t + 256 u holds row e >> 3, k 4 (e & 7) .. +3.
+// KR: M[k][r], thread e holds k e >> 4, rows 4 (e & 15) .. +3.  Elements outside
+// r < rmax, k < kmax are 0 (masked at the store, as blk_fix).
+struct Blk2 {
+  v4f v[2];
+};
+struct Blk2Bounds {
+  int64_t r0, rmax, k0, kmax;
+};
+template <bool RK>
+__device__ __forceinline__ int blk2_nv(const Blk2Bounds& k, int u) {
+  const int e = threadIdx.x + 256 * u;
+  if constexpr (RK) {
+    const int64_t r = k.r0 + (e >> 3), c = k.k0 + 4 * (e & 7);
+    return r < k.rmax ? (int)min(max(k.kmax - c, (int64_t)0), (int64_t)4) : 0;
+  } else {
+    const int64_t kk = k.k0 + (e >> 4), r = k.r0 + 4 * (e & 15);
+    return kk < k.kmax ? (int)min(max(k.rmax - r, (int64_t)0), (int64_t)4) : 0;
+  }
+}
+template <bool RK>
+__device__ __forceinline__ void blk2_load(Blk2& s, const float* __restrict__ M, int64_t ld, const Blk2Bounds& k) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    v4f x = {0.f, 0.f, 0.f, 0.f};
+    if (blk2_nv<RK>(k, u) > 0)
+      x = RK ? *(const v4f*)(M + (k.r0 + (e >> 3)) * ld + k.k0 + 4 * (e & 7))    // rows padded to 4
+             : *(const v4f*)(M + (k.k0 + (e >> 4)) * ld + k.r0 + 4 * (e & 15));
+    s.v[u] = x;
+  }
+}
+// mask, split into the three planes P[3][GX_PL] and store; csp (KR only) += the
+// masked values per row of the thread's four
+template <bool RK, bool CS>
+__device__ __forceinline__ void blk2_store(Blk2& s, const Blk2Bounds& k, __bf16* P, double (&csp)[4]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int nv = blk2_nv<RK>(k, u);
+    v4f x = s.v[u];
+    if (nv < 1) x.x = 0.f;
+    if (nv < 2) x.y = 0.f;
+    if (nv < 3) x.z = 0.f;
+    if (nv < 4) x.w = 0.f;
+    bf16x4 h4, m4, l4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      __bf16 hh, mm, ll;
+      split3(x[c], hh, mm, ll);
+      h4[c] = hh;
+      m4[c] = mm;
+      l4[c] = ll;
+      if constexpr (CS) csp[c] += (double)x[c];
+    }
+    const int off = RK ? (e >> 3) * GX_RK + 4 * (e & 7) : (e >> 4) * GX_KR + 4 * (e & 15);
+    *(bf16x4*)&P[off] = h4;
+    *(bf16x4*)&P[GX_PL + off] = m4;
+    *(bf16x4*)&P[2 * GX_PL + off] = l4;
+  }
+}
+// the bf16x8 fragment (MFMA rows rb .. rb + 15, K slots 8 lq .. 8 lq + 7) of plane pl
+template <bool RK>
+__device__ __forceinline__ bf16x8 frag3(const __bf16* P, int pl, int rb, int li, int lq) {
+  if constexpr (RK) {
+    return *(const bf16x8*)&P[pl * GX_PL + (rb + li) * GX_RK + 8 * lq];
+  } else {
+    const int tq = li >> 2, tp = li & 3;
+    return tr16_pair(&P[pl * GX_PL + (8 * lq + tq) * GX_KR + rb + 4 * tp],
+                     &P[pl * GX_PL + (8 * lq + 4 + tq) * GX_KR + rb + 4 * tp]);
+  }
+}
+}  // namespace
+
+template <int PH>
+__global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
+    k_gx_gemm_x3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
+                 int total, int per) {
+  constexpr bool ARK = PH != GX_GRAD;  // A staged [row][k]
+  constexpr bool BRK = PH == GX_FWD;   // B staged [row][k]
+  constexpr bool F64 = PH == GX_GRAD;
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * GX_PL];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * GX_PL];
+  __shared__ double cs_s[16][GX_T];
+  const int q = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD-aware numbering (k_gx_gemm)
+  if (q >= total) return;
+  int lo_ = 0, hi_ = nb;
+  while (hi_ - lo_ > 1) {
+    const int mid = (lo_ + hi_) >> 1;
+    if (prefix[mid] <= q) lo_ = mid;
+    else hi_ = mid;
+  }
+  const int b = blist[lo_];
+  const BranchDev& bd = st.br[b];
+  int tmc, tnc, ns;
+  gx_dims(st, bd, PH, l, tmc, tnc, ns);
+  int r = q - prefix[lo_];
+  const int split = r / (tmc * tnc);
+  r -= split * tmc * tnc;
+  const int tm = r / tnc, tn = r % tnc;
+  const int64_t rows = gx_rows(st);
+  float* S = gx_base(st, bd);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int li = lane & 15, lq = lane >> 4;
+  const int ar = 32 * (wv >> 1), bc = 32 * (wv & 1);
+
+  int64_t kb0 = 0, kb1, kcount;
+  const float* Am;
+  const float* Bm;
+  int64_t lda, ldb;
+  int wi = 0, wo;
+  if constexpr (PH == GX_FWD) {  // Z_l = A_{l-1} Wp_l^T: A [individual][in], B = Wp_l [out][in]
+    kcount = bd.widths[l - 1];
+    Am = S + bd.gx_a[l - 1];
+    lda = bd.gx_ld[l - 1];
+    Bm = S + bd.gx_w[l];
+    ldb = bd.gx_wld[l];
+    wo = bd.widths[l];
+  } else if constexpr (PH == GX_BWD) {  // delta_l Wp_l: A = delta_l [individual][out], B = Wp_l [out = k][in]
+    kcount = bd.widths[l];
+    Am = S + bd.gx_h[l];
+    lda = bd.gx_ld[l];
+    Bm = S + bd.gx_w[l];
+    ldb = bd.gx_wld[l];
+    wo = bd.widths[l - 1];
+  } else {  // GRAD: dW_l = A_{l-1}^T delta_l over the split's rows (K = individuals)
+    const int ntile = (st.nfrag + 3) / 4;
+    kcount = rows;
+    Am = S + bd.gx_a[l - 1];
+    lda = bd.gx_ld[l - 1];
+    wi = bd.widths[l - 1];
+    Bm = S + bd.gx_h[l];
+    ldb = bd.gx_ld[l];
+    wo = bd.widths[l];
+    kb0 = 2 * ((int64_t)ntile * split / ns);  // 64-row tiles -> 32-deep K blocks
+    kb1 = 2 * ((int64_t)ntile * (split + 1) / ns);
+  }
+  if constexpr (PH != GX_GRAD) kb1 = (kcount + GX_KB - 1) / GX_KB;
+  // the operand blocks of K block kb: rows of the A block are output rows (64 tm ..),
+  // rows of the B block output columns (64 tn ..)
+  auto bnd_a = [&](int64_t kb) {
+    return Blk2Bounds{64 * (int64_t)tm, PH == GX_GRAD ? (int64_t)wi : rows, GX_KB * kb, kcount};
+  };
+  auto bnd_b = [&](int64_t kb) { return Blk2Bounds{64 * (int64_t)tn, (int64_t)wo, GX_KB * kb, kcount}; };
+  Blk2 ra, rb;
+  double csa[4] = {0.0, 0.0, 0.0, 0.0}, csp[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD: column sums of delta_l
+  // FWD / BWD: B = Wp_l from its pre-split planes [3][out][r32(in)] (k_gx_prep): one
+  // 16-byte piece of 8 elements per plane and thread, copied to the stage as is.
+  // FWD stages it [out][in] (thread: out row t >> 2, in 8 (t & 3) ..), BWD [out = k][in]
+  // (thread: out row t >> 3, in 8 (t & 7) ..); rows past the layer and pieces past
+  // the in width are zero (the planes' padding covers the rest of a piece)
+  constexpr bool BP = PH != GX_GRAD;
+  v4i rbp[3];
+  const __bf16* Wp3 = BP ? reinterpret_cast<const __bf16*>(S + bd.gx_wp[l]) : nullptr;
+  const int64_t l3 = BP ? ((bd.win[l] + 31) & ~31) : 0, p3 = BP ? (int64_t)bd.widths[l] * l3 : 0;
+  auto load_bp = [&](v4i (&rp_)[3], int64_t kb) {
+    int64_t row, col;
+    bool ok;
+    if constexpr (PH == GX_FWD) {
+      row = 64 * (int64_t)tn + (t >> 2);
+      col = GX_KB * kb + 8 * (t & 3);
+      ok = row < wo;
+    } else {
+      row = GX_KB * kb + (t >> 3);
+      col = 64 * (int64_t)tn + 8 * (t & 7);
+      ok = row < kcount && col < wo;
+    }
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      rp_[pl] = ok ? *reinterpret_cast<const v4i*>(Wp3 + pl * p3 + row * l3 + col) : v4i{0, 0, 0, 0};
+  };
+  auto store_bp = [&](v4i (&rp_)[3]) {
+    const int off = PH == GX_FWD ? (t >> 2) * GX_RK + 8 * (t & 3) : (t >> 3) * GX_KR + 8 * (t & 7);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<v4i*>(&Bs[pl * GX_PL + off]) = rp_[pl];
+  };
+  const bool want_cs = PH == GX_GRAD && tm == 0;
+
+  v4f acc[4];
+  double dacc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
+  }
+  auto load = [&](int64_t kb) {
+    blk2_load<ARK>(ra, Am, lda, bnd_a(kb));
+    if constexpr (BP) load_bp(rbp, kb);
+    else blk2_load<BRK>(rb, Bm, ldb, bnd_b(kb));
+  };
+  if (kb0 < kb1) load(kb0);
+  for (int64_t kb = kb0; kb < kb1; ++kb) {
+    blk2_store<ARK, false>(ra, bnd_a(kb), As, csa);
+    if constexpr (BP) store_bp(rbp);
+    else if (want_cs) blk2_store<BRK, true>(rb, bnd_b(kb), Bs, csp);
+    else blk2_store<BRK, false>(rb, bnd_b(kb), Bs, csp);
+    __syncthreads();
+    if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int X = 0; X < 2; ++X)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[X][pl] = frag3<ARK>(As, pl, ar + 16 * X, li, lq);
+#pragma unroll
+    for (int Y = 0; Y < 2; ++Y) {
+      bf16x8 bq[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bq[pl] = frag3<BRK>(Bs, pl, bc + 16 * Y, li, lq);
+#pragma unroll
+      for (int X = 0; X < 2; ++X) {
+        v4f& c = acc[2 * X + Y];
+        // small products first
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][2], bq[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][1], bq[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][0], bq[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][1], bq[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][0], bq[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][0], bq[0], c, 0, 0, 0);
+      }
+    }
+    if constexpr (F64) {
+      if (kb & 1) {  // f64 across 64-deep K
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          dacc[x][0] += (double)acc[x].x;
+          dacc[x][1] += (double)acc[x].y;
+          dacc[x][2] += (double)acc[x].z;
+          dacc[x][3] += (double)acc[x].w;
+          acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+    __syncthreads();  // every wave is done with the stage before it is refilled
+  }
+  if constexpr (F64) {  // an odd block count leaves one block in acc
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      dacc[x][0] += (double)acc[x].x;
+      dacc[x][1] += (double)acc[x].y;
+      dacc[x][2] += (double)acc[x].z;
+      dacc[x][3] += (double)acc[x].w;
+    }
+  }
+  double cs = 0.0;
+  if (want_cs) {  // 16 threads per 4-column group, added in thread order (deterministic)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) cs_s[t >> 4][4 * (t & 15) + x] = csp[x];
+    __syncthreads();
+    if (t < GX_T)
+      for (int k = 0; k < 16; ++k) cs += cs_s[k][t];
+  }
+  gx_epilogue<PH, F64>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, nullptr);
+}
+
+// ---------------------------------------------------------------------------
 // PREP: padded weights, W0 / sigma, c0 = b0 - mu^T (W0 / sigma) (f64), biases
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __restrict__ blist) {
+  // grid (branches, GX_PREP_Y): every element is independent (computed from theta),
+  // so the y blocks of a branch split every loop below
   const int b = blist[blockIdx.x];
   const BranchDev& bd = st.br[b];
   float* S = gx_base(st, bd);
   const float* th = st.theta + bd.p_off;
   const float* mu = st.mu + bd.mk_off;
   const float* sg = st.sigma + bd.mk_off;
-  for (int l = 0; l < bd.L; ++l) {
-    const int win = bd.win[l], wo = bd.widths[l], ld = bd.gx_wld[l];
+  const int64_t g0 = (int64_t)blockIdx.y * 256 + threadIdx.x, gs = (int64_t)gridDim.y * 256;
+  auto wval = [&](int l, int k, int j) -> float {  // Wp_l[k][j]: W_l (layer 0: W0 / sigma), 0 past the in width
+    if (j >= bd.win[l]) return 0.f;
+    const float v = th[bd.woff[l] + (int64_t)k * bd.win[l] + j];
+    return l == 0 ? (sg[j] > 0.f ? v / sg[j] : 0.f) : v;
+  };
+  for (int l = 0; l < bd.L; ++l) {  // padded weights [out][gx_wld[l]]
+    const int ld = bd.gx_wld[l];
     float* Wp = S + bd.gx_w[l];
-    const float* W = th + bd.woff[l];
-    const int64_t tot = (int64_t)wo * ld;
-    for (int64_t e = threadIdx.x; e < tot; e += 256) {
-      const int k = (int)(e / ld), j = (int)(e - (int64_t)k * ld);
-      float v = 0.f;
-      if (j < win) {
-        v = W[(int64_t)k * win + j];
-        if (l == 0) v = sg[j] > 0.f ? v / sg[j] : 0.f;
-      }
-      Wp[e] = v;
-    }
+    const int64_t tot = (int64_t)bd.widths[l] * ld;
+    for (int64_t e = g0; e < tot; e += gs) Wp[e] = wval(l, (int)(e / ld), (int)(e % ld));
   }
-  __syncthreads();
   {  // W0 / sigma as three bf16 planes [3][w0][64 nchunks], zero padded (k_gx_gemm_b3)
-    const int w0 = bd.widths[0], m64 = 64 * bd.nchunks, ld = bd.gx_wld[0];
-    const float* Wp = S + bd.gx_w[0];
+    const int m64 = 64 * bd.nchunks;
     __bf16* P3 = reinterpret_cast<__bf16*>(S + bd.gx_w0p);
-    const int64_t tot = (int64_t)w0 * m64;
-    for (int64_t e = threadIdx.x; e < tot; e += 256) {
-      const int k = (int)(e / m64), j = (int)(e - (int64_t)k * m64);
-      __bf16 hh = (__bf16)0.f, mm = (__bf16)0.f, ll = (__bf16)0.f;
-      if (j < bd.m) split3(Wp[(int64_t)k * ld + j], hh, mm, ll);
+    const int64_t tot = (int64_t)bd.widths[0] * m64;
+    for (int64_t e = g0; e < tot; e += gs) {
+      __bf16 hh, mm, ll;
+      split3(wval(0, (int)(e / m64), (int)(e % m64)), hh, mm, ll);
       P3[e] = hh;
       P3[tot + e] = mm;
       P3[2 * tot + e] = ll;
     }
   }
-  // c0 (one thread per unit, f64 in marker order) and the other biases
+  for (int l = 1; l < bd.L - 1; ++l) {  // Wp_l as three bf16 planes [3][w_l][r32(win_l)], zero padded (k_gx_gemm_x3)
+    const int l3 = (bd.win[l] + 31) & ~31;
+    __bf16* P3 = reinterpret_cast<__bf16*>(S + bd.gx_wp[l]);
+    const int64_t tot = (int64_t)bd.widths[l] * l3;
+    for (int64_t e = g0; e < tot; e += gs) {
+      __bf16 hh, mm, ll;
+      split3(wval(l, (int)(e / l3), (int)(e % l3)), hh, mm, ll);
+      P3[e] = hh;
+      P3[tot + e] = mm;
+      P3[2 * tot + e] = ll;
+    }
+  }
+  // c0 = b0 - sum_j mu_j Wp_0[k][j] (f64): one wave per unit, lane-strided partials
+  // added in a fixed order; the other biases
   {
-    const int m = bd.m, ld = bd.gx_wld[0];
-    const float* Wp = S + bd.gx_w[0];
-    for (int k = threadIdx.x; k < bd.widths[0]; k += 256) {
+    const int lane = threadIdx.x & 63;
+    const int gw = (int)blockIdx.y * 4 + (threadIdx.x >> 6), nw = (int)gridDim.y * 4;
+    for (int k = gw; k < bd.widths[0]; k += nw) {
       double acc = 0.0;
-      for (int j = 0; j < m; ++j) acc += (double)mu[j] * (double)Wp[(int64_t)k * ld + j];
-      S[bd.gx_b[0] + k] = (float)((double)th[bd.boff[0] + k] - acc);
+      for (int j = lane; j < bd.m; j += 64) acc += (double)mu[j] * (double)wval(0, k, j);
+      acc = wave_sum_d(acc);
+      if (lane == 0) S[bd.gx_b[0] + k] = (float)((double)th[bd.boff[0] + k] - acc);
     }
   }
   for (int l = 1; l < bd.L - 1; ++l)
-    for (int k = threadIdx.x; k < bd.widths[l]; k += 256) S[bd.gx_b[l] + k] = th[bd.boff[l] + k];
+    for (int64_t k = g0; k < bd.widths[l]; k += gs) S[bd.gx_b[l] + k] = th[bd.boff[l] + k];
 }
 
 // ---------------------------------------------------------------------------
@@ -809,7 +1104,7 @@ __global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t*
 // launchers
 // ---------------------------------------------------------------------------
 void launch_gx_prep(const DevState& st, const int32_t* blist, int nb, hipStream_t s) {
-  if (nb > 0) hipLaunchKernelGGL(k_gx_prep, dim3(nb), dim3(256), 0, s, st, blist);
+  if (nb > 0) hipLaunchKernelGGL(k_gx_prep, dim3(nb, GX_PREP_Y), dim3(256), 0, s, st, blist);
 }
 void launch_gx_head(const DevState& st, const int32_t* blist, int nb, int max_splits, hipStream_t s) {
   if (nb <= 0) return;
@@ -830,6 +1125,14 @@ void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, con
   if (!exact && ph == GX_GRAD0) {
     hipLaunchKernelGGL(k_gx_gemm_b3<GX_GRAD0>, g, blk, 0, s, st, blist, prefix, nb, total, per);
     return;
+  }
+  if (!exact) {
+    switch (ph) {
+      case GX_FWD: hipLaunchKernelGGL(k_gx_gemm_x3<GX_FWD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); return;
+      case GX_BWD: hipLaunchKernelGGL(k_gx_gemm_x3<GX_BWD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); return;
+      case GX_GRAD: hipLaunchKernelGGL(k_gx_gemm_x3<GX_GRAD>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); return;
+      default: break;
+    }
   }
   switch (ph) {
     case GX_FWD0: hipLaunchKernelGGL(k_gx_gemm<GX_FWD0>, g, blk, 0, s, st, blist, prefix, nb, l, total, per); break;

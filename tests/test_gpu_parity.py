@@ -610,9 +610,11 @@ def test_default_arch_full_n(Ctx):
 
 @pytest.mark.parametrize("exact", ["0", "1"])
 def test_layered_masked_layer_modes(Ctx, exact):
-    """gx's masked layer on the bf16 MFMA (genotype codes exact, the f32 operand as
-    three bf16 planes; default) and on the f32 MFMA (BANN_GX_EXACT=1): both within
-    the 1e-5 tolerance on a default-architecture branch with several row splits."""
+    """gx's GEMMs on the bf16 MFMA (default: the masked layer with the genotype codes
+    exact and the f32 operand as three bf16 planes; the hidden layers with both f32
+    operands as three planes and the six leading plane products) and on the f32
+    MFMA (BANN_GX_EXACT=1): both within the 1e-5 tolerance on a default-architecture
+    branch with several row splits."""
     cfg = dict(n=9000, m=300, widths=[150, 150, 1], act="tanh", prior="ridge_ard")
     rng, g, snps, br = make_problem(cfg, 47)
     os.environ["BANN_GX_EXACT"] = exact
