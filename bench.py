@@ -338,11 +338,15 @@ def main():
                           "peak": BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF, "unit": "TFLOP/s",
                           "frac": hidden_flops / (grad_ms * 1e-3) / 1e12 /
                           (BF16_MFMA_PEAK_TF if args.hidden_bf16 else F32_MFMA_PEAK_TF),
-                          "basis": ("GEMM flops 4 n m W + 6 n W S per branch per launch (the whole gradient "
-                                    "evaluation: FWD0, FWD1, BWD1, GRAD1, GRAD0) against the f32 MFMA peak; the "
-                                    "masked layer (4 n m W) runs on bf16 MFMA with the f32 operand as three bf16 "
-                                    "planes (BANN_GX_EXACT=1: f32 MFMA), the hidden layers on f32 MFMA") if path == "layered" else
+                          "basis": ("f32-equivalent GEMM flops 4 n m W + 6 n W S per branch per launch (the whole "
+                                    "gradient evaluation: FWD0, FWD1, BWD1, GRAD1, GRAD0) against the f32 MFMA peak "
+                                    "(the parity-exact BANN_GX_EXACT=1 path's ceiling); executed on the bf16 MFMA: "
+                                    "the masked layer with the f32 operand as three bf16 planes (3 products), the "
+                                    "hidden layers with both operands as three planes (6 products), see "
+                                    "bf16_pipe_frac") if path == "layered" else
                                    "hidden-layer GEMM flops 6 n W S per branch per launch",
+                          **({"bf16_pipe_frac": (3 * 2 * 2 * n * m_b * widths[0] + 6 * 3 * 2 * n * widths[0] * widths[1])
+                              * nb / (grad_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF} if path == "layered" else {}),
                           "i8_mfma_tops": i8_ops / (grad_ms * 1e-3) / 1e12,
                           "mfma_busy_pmc": (mfma_pmc or {}).get("mfma_busy_per_simd_cycle"),
                           "hbm_GBps": achieved} if wide else
