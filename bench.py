@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--step-factor", type=float, default=None,
-                    help="Izmailov factor c; default 1.0 (cli.rs:99-100), 0.15 for c5, 0.02 for c3def (wide branches: acceptance > 0.6)")
+                    help="Izmailov factor c; default 1.0 (cli.rs:99-100), 0.1 for c5, 0.02 for c3def (wide branches: acceptance > 0.6 at L = 100)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-branches", type=int, default=None)   # default 96 (c3def: 4), capped at the branch count
     ap.add_argument("--cpu-sample-steps", type=int, default=None)      # default 16 (c3def: 2)
@@ -133,8 +133,8 @@ def main():
     n, M_total, B_total, widths = CONFIGS[args.config]
     if args.step_factor is None:
         # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
-        # curvature, c = 1 rejects every trajectory; c = 0.15 accepts ~0.7
-        args.step_factor = {"c5": 0.15, "c3def": 0.02}.get(args.config, 1.0)
+        # curvature, c = 1 rejects every trajectory; c = 0.1 accepts ~0.9 at L = 100 (tools/gpu_c5sweep.sh)
+        args.step_factor = {"c5": 0.1, "c3def": 0.02}.get(args.config, 1.0)
     heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
     if args.cpu_sample_branches is None:
         args.cpu_sample_branches = 4 if heavy else 96
@@ -173,10 +173,7 @@ def main():
     out_prec = tot[1] / tot[0]
     fsum = np.zeros(n, np.float64)
     for k in range(nb):
-        prec = precs[k]
-        prec[len(widths) - 1] = np.array([out_prec])
         ctx.set_params(k, params[k])
-        ctx.set_precisions(k, np.concatenate(prec).astype(np.float32))
     preds = ctx.predict_many(list(range(nb)))   # one packed launch
     fsum += preds.sum(axis=0, dtype=np.float64)
     if dist is not None:
@@ -186,7 +183,15 @@ def main():
         fsum = tt.cpu().numpy()
     # phenotype y = sum_b f_b + noise at h^2 = 0.5; residual = noise; each branch
     # is fitted to its partial residual residual + f_b (net.rs:279-280)
-    noise = np.random.default_rng(7).normal(0.0, max(float(np.std(fsum)), 1e-3), size=n)
+    # residual noise at the error precision's default 2.0 (branch_cfg_builder.rs:394):
+    # Var(noise) = 1 / 2, the value the error precision's Gibbs draw
+    # (sample_error_precision, net.rs:272) is consistent with, whatever the summed
+    # output's scale (a W = 250 cohort's sum is ~40x a W = 4 one's)
+    noise = np.random.default_rng(7).normal(0.0, math.sqrt(0.5), size=n)
+    for k in range(nb):
+        prec = precs[k]
+        prec[len(widths) - 1] = np.array([out_prec])
+        ctx.set_precisions(k, np.concatenate(prec).astype(np.float32))
     for k in range(nb):
         ctx.set_target(k, (noise + preds[k]).astype(np.float32))
     del preds
