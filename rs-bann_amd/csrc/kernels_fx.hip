@@ -77,49 +77,30 @@ __device__ __forceinline__ float comb4(v4i d) {  // sum_d D_d 2^(-7 d)
   return (float)d[0] + (float)d[1] * 0x1p-7f + (float)d[2] * 0x1p-14f + (float)d[3] * 0x1p-21f;
 }
 
-// 2^21 x value of digit sums G, rounded once: the low digit sums grow past 2^24
-// over an item's tiles (in-place fields weigh up to 48), where comb4's
+// delta0 digits: V = rint(x 2^e), |V| < 2^27, as four signed 8-bit digits
+// V = d0 + d1 2^8 + d2 2^16 + d3 2^24 (byte d = digit d, d0..d2 in [-128, 127],
+// d3 in [-8, 8]): offsetting the three low bytes by 128 and flipping their top
+// bits is the whole recoding, 2 VALU
+__device__ __forceinline__ uint32_t digits4_fx(float x, int e) {
+  const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
+  return ((uint32_t)V + 0x00808080u) ^ 0x00808080u;
+}
+
+// value(G) of digit sums G (digit d weighs 2^(8 d)), rounded once: the digit sums
+// grow past 2^24 over an item's tiles (in-place fields weigh up to 48), where a
 // per-digit float conversion would round each one
 __device__ __forceinline__ float comb4_exact(v4i G) {
-  const int64_t N = ((int64_t)G[0] << 21) + ((int64_t)G[1] << 14) + ((int64_t)G[2] << 7) + (int64_t)G[3];
+  const int64_t N = (int64_t)G[0] + ((int64_t)G[1] << 8) + ((int64_t)G[2] << 16) + ((int64_t)G[3] << 24);
   return (float)N;
 }
 
-// value(G) * 2^-sh for digit sums G (digit d weighs 2^(-7 d)), sh >= 0: form
-// N = G0 2^21 + G1 2^14 + G2 2^7 + G3 in int64 (|G_d| < 2^24), shift it, and
-// re-split into 7-bit digits (exact up to the dropped low bits, < 2^-21 of the
-// new unit).  Branch- and loop-free so the accumulators are updated in place.
+// value(G) * 2^-sh for digit sums G, sh >= 0: form N in int64 (|G_d| < 2^31),
+// shift it, and re-split into 8-bit digits (exact up to the dropped low bits, < 1
+// of the new unit).  Branch- and loop-free so the accumulators are updated in place.
 __device__ __forceinline__ v4i shr_digits(v4i G, int sh) {
-  const int64_t N = ((int64_t)G[0] << 21) + ((int64_t)G[1] << 14) + ((int64_t)G[2] << 7) + (int64_t)G[3];
+  const int64_t N = (int64_t)G[0] + ((int64_t)G[1] << 8) + ((int64_t)G[2] << 16) + ((int64_t)G[3] << 24);
   const int64_t M = N >> (sh < 63 ? sh : 63);
-  return v4i{(int)(M >> 21), (int)((M >> 14) & 127), (int)((M >> 7) & 127), (int)(M & 127)};
-}
-
-// signed digits of V = rint(v 2^21), |v| < 64:  V = d0 2^21 + d1 2^14 + d2 2^7 + d3,
-// d0 in [-64, 64], d1..d3 in [0, 127]; packed little-endian (byte d = digit d)
-__device__ __forceinline__ uint32_t digits4_fx(float x, int e) {
-  const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
-  const uint32_t u = (uint32_t)V;
-#if BANN_ABLATE & 16384
-  uint32_t w = __builtin_amdgcn_ubfe(u, 21, 8);
-  w |= __builtin_amdgcn_ubfe(u, 14, 7) << 8;
-  w |= __builtin_amdgcn_ubfe(u, 7, 7) << 16;
-  w |= (u & 127u) << 24;
-  return w;
-#else
-  // three bfe + three v_lshl_or_b32 + one and (the compiler's mask form takes 8)
-  uint32_t w, t;
-  asm("v_bfe_u32 %0, %2, 21, 8\n\t"
-      "v_bfe_u32 %1, %2, 14, 7\n\t"
-      "v_lshl_or_b32 %0, %1, 8, %0\n\t"
-      "v_bfe_u32 %1, %2, 7, 7\n\t"
-      "v_lshl_or_b32 %0, %1, 16, %0\n\t"
-      "v_and_b32 %1, 0x7f, %2\n\t"
-      "v_lshl_or_b32 %0, %1, 24, %0"
-      : "=&v"(w), "=&v"(t)
-      : "v"(u));
-  return w;
-#endif
+  return v4i{(int)(M & 255), (int)((M >> 8) & 255), (int)((M >> 16) & 255), (int)(M >> 24)};
 }
 
 __device__ __forceinline__ void swap32(float& a, float& b) {
@@ -173,7 +154,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   const int64_t n = st.n;
   const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
 
-  // ---- branch constants: head weights (LDS, read per tile as broadcasts), W0 digits, column scale ----
+  // ---- branch constants: head weights (LDS, then scalar registers), W0 digits, column scale ----
   const float* th = st.theta + bd.p_off;
   for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
     const int l = t / 20, r = t - l * 20;
