@@ -6,6 +6,6 @@ for r in $(seq ${REPS:-2}); do
   for a in base $VARIANTS; do
     LIBV=""; [ "$a" != base ] && LIBV=rs-bann_amd/abl/librsbann_amd_abl$a.so
     BANN_LIB=$LIBV timeout -k 10 90 python tools/kbench.py --branches 1000 --iters ${ITERS:-30} --tag c3-$a || exit 1
-    [ -n "$C2" ] && { BANN_LIB=$LIBV timeout -k 10 90 python tools/kbench.py --branches 64 --n 10000 --m 2000 --iters ${ITERS:-30} --tag c2-$a || exit 1; }
+    if [ -n "$C2" ]; then BANN_LIB=$LIBV timeout -k 10 90 python tools/kbench.py --branches 64 --n 10000 --m 2000 --iters ${ITERS:-30} --tag c2-$a || exit 1; fi
   done
 done
