@@ -15,6 +15,7 @@
 // second half step of step k.  Partial sums from the gradient kernels are
 // combined here in a fixed order (deterministic).
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -499,6 +500,8 @@ void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int3
   if (nb <= 0) return;
   if (large)
     hipLaunchKernelGGL((k_update<UPD_THREADS_L, 4>), dim3(nb), dim3(UPD_THREADS_L), 0, s, st, branches, mode, step);
+  else if (getenv("BANN_UPD512") && atoi(getenv("BANN_UPD512")))
+    hipLaunchKernelGGL((k_update<512, 1>), dim3(nb), dim3(512), 0, s, st, branches, mode, step);
   else
     hipLaunchKernelGGL((k_update<UPD_THREADS, 2>), dim3(nb), dim3(UPD_THREADS), 0, s, st, branches, mode, step);
 }
