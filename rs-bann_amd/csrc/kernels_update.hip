@@ -494,13 +494,14 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
   }
 }
 
-// small: branches with P <= 2048 and m <= 512 (256 threads); large: the rest (1024 threads)
+// small: branches with P <= 2048 and m <= 512 (256 threads; 512 when the launch has at most
+// one branch per CU: N = 8 shard 0.0163 -> 0.0129 ms); large: the rest (1024 threads)
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
                    hipStream_t s, int large) {
   if (nb <= 0) return;
   if (large)
     hipLaunchKernelGGL((k_update<UPD_THREADS_L, 4>), dim3(nb), dim3(UPD_THREADS_L), 0, s, st, branches, mode, step);
-  else if (getenv("BANN_UPD512") && atoi(getenv("BANN_UPD512")))
+  else if (nb <= 256)  // at most one workgroup per CU: 512 threads, more loads in flight per branch
     hipLaunchKernelGGL((k_update<512, 1>), dim3(nb), dim3(512), 0, s, st, branches, mode, step);
   else
     hipLaunchKernelGGL((k_update<UPD_THREADS, 2>), dim3(nb), dim3(UPD_THREADS), 0, s, st, branches, mode, step);
