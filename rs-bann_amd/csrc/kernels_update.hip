@@ -156,6 +156,10 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   const int P = bd.P, m = bd.m, w0 = bd.widths[0];
   const int64_t base = bd.p_off;
   const int t = threadIdx.x;
+  // a finished trajectory (STEP / LAST after an early rejection) is left alone; the
+  // status is checked after every load of the step has been issued, not before
+  const bool check = !prof && (mode == MODE_STEP || mode == MODE_LAST);
+  const int status = st.status[b];
   // marker statistics for the refresh, prefetched
   float mus[MPT], sgs[MPT];
 #pragma unroll
@@ -186,7 +190,6 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     const float sgn = th[c] > 0.f ? 1.f : (th[c] < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
     const float reg = lasso ? lm * sgn : lm * th[c];
     gr[c] = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
-    if (!prof) st.grad[base + i] = gr[c];
     sums[0] -= lasso ? (double)ll * fabs((double)th[c]) : 0.5 * (double)ll * (double)th[c] * (double)th[c];
     if (mode == MODE_INIT) {
       sums[1] += (double)pm[c] * (double)pm[c];
@@ -196,6 +199,11 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
       sums[2] += ((double)th[c] - (double)t0[c]) * (double)pm[c];
     }
   }
+  if (check && status != ST_RUNNING) return;
+  if (!prof)
+#pragma unroll
+    for (int c = 0; c < UPD_CAP; ++c)
+      if (t + c * NT < P) st.grad[base + t + c * NT] = gr[c];
   if (mode == MODE_GRAD) {
     double v1[1] = {sums[0]};
     block_sum_n<NT, 1>(v1, redd);
@@ -378,12 +386,12 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
     }
     return;
   }
-  if (!prof && (mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
   if ((bd.fused == 1 || bd.fused == 3) && P <= UPD_CAP * NT && bd.m <= MPT * NT && bd.widths[0] <= 4) {
     __shared__ float s_th[UPD_CAP * NT];
-    update_small<NT, MPT>(st, b, bd, mode, prof, step, redd, s_th);
+    update_small<NT, MPT>(st, b, bd, mode, prof, step, redd, s_th);  // checks the status itself
     return;
   }
+  if (!prof && (mode == MODE_STEP || mode == MODE_LAST) && st.status[b] != ST_RUNNING) return;
 
   // ---- rss (fixed-order split reduction) ----
   double rss = 0.0;
