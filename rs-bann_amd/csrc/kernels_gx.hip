@@ -14,6 +14,8 @@
 //           c0 = b0 - sum_j mu_j Wp_0[.][j] (f64): standardisation folded into W0
 //   FWD0    Z0 = G Wp_0^T + c0 (G decoded from the 2-bit tile image)   -> A0 = h(Z0), H0 = h'(Z0)
 //   FWD l   Z_l = A_{l-1} Wp_l^T + b_l                                  -> A_l, H_l
+//           (H_l = h'(Z_l) is stored for SiLU only: for tanh, ReLU, leaky ReLU and
+//           identity h' is a function of A_l, formed where it is used)
 //   HEAD    out = A_s w_out (775-782), e = out - y, rss (823-828), pred,
 //           dW_out = A_s^T e (830-835), delta_s = H_s * e w_out (844-847, in place over H_s)
 //   BWD l   delta_{l-1} = H_{l-1} * (delta_l Wp_l)          (855-861, in place over H_{l-1})
@@ -177,6 +179,19 @@ __device__ __forceinline__ void geno_store_mi(uint32_t g, float* L) {
 
 }  // namespace
 
+// h'(z) as a function of a = h(z) for the activations where it is one (tanh:
+// 1 - a^2; ReLU / leaky ReLU: a > 0 <=> z > 0; identity): those layers store A_l
+// only, and the backward phases form H_l from it (SiLU keeps H_l)
+__device__ __forceinline__ bool dh_from_a(int act) { return act != 3; }
+__device__ __forceinline__ float act_dh_a(float a, int act) {
+  switch (act) {
+    case 0: return 1.f - a * a;
+    case 1: return a > 0.f ? 1.f : 0.f;
+    case 2: return a > 0.f ? 1.f : (a < 0.f ? 0.01f : 0.f);
+    default: return 1.f;
+  }
+}
+
 // the epilogue of a 64 x 64 output tile: lane holds rows ar + 16 X + 4 lq + y and
 // columns bc + 16 Y + li of accumulator x = 2 X + Y (f32 acc, or the f64 dacc when
 // F64).  FWD0 / FWD: A = h(Z + b), H = h'(Z + b); BWD: delta_{l-1} = H * acc in
@@ -208,7 +223,7 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
           const float z = (F64 ? (float)dacc[x][y] : acc[x][y]) + bj;  // mid_layer_pre_activation: matmul + bias
           const float a = ACT == 0 ? fast_tanh(z) : act_h_t<ACT>(z);  // tanh to ~2 ulp (layer outputs feed GEMMs)
           Ao[row * ld + j] = a;
-          Ho[row * ld + j] = act_dh_t<ACT>(z, a);
+          if constexpr (ACT == 3) Ho[row * ld + j] = act_dh_t<ACT>(z, a);
         }
       }
     };
@@ -221,7 +236,10 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     }
   } else if constexpr (PH == GX_BWD) {
     float* Hd = S + bd.gx_h[l - 1];
+    const float* Ad = S + bd.gx_a[l - 1];
     const int64_t ld = bd.gx_ld[l - 1];
+    const int act = bd.act;
+    const bool fa = dh_from_a(act);
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int j = 64 * tn + bc + 16 * (x & 1) + li;
@@ -229,7 +247,8 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
         const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
-        Hd[row * ld + j] *= acc[x][y];  // delta = h'(z) * (delta_next W^T)
+        const float h = fa ? act_dh_a(Ad[row * ld + j], act) : Hd[row * ld + j];
+        Hd[row * ld + j] = h * acc[x][y];  // delta = h'(z) * (delta_next W^T)
       }
     }
   } else {
@@ -1060,6 +1079,8 @@ __global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __r
   if (lane == 0) r_s[wv] = rss;
   __syncthreads();
   double* dwo = (double*)(S + bd.gx_dwo) + (int64_t)tile * Sw;
+  const int act = bd.act;
+  const bool fa = dh_from_a(act);
   for (int k = t; k < Sw; k += 256) {
     const float wk = wout[k];
     double d = 0.0;
@@ -1067,8 +1088,10 @@ __global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __r
     for (int i = 0; i < GX_T; ++i) {
       const float ei = e_s[i];
       const int64_t o = (r0 + i) * ld + k;
-      d += (double)A[o] * (double)ei;
-      H[o] *= ei * wk;  // delta_s = h'(z_s) * (e w_out^T)
+      const float a_o = A[o];
+      d += (double)a_o * (double)ei;
+      const float h = fa ? act_dh_a(a_o, act) : H[o];
+      H[o] = h * (ei * wk);  // delta_s = h'(z_s) * (e w_out^T)
     }
     dwo[k] = d;
   }
