@@ -22,7 +22,8 @@
 #include "bann_internal.h"
 #include "rng.h"
 
-#define UPD_THREADS 256   // small branches (P <= 2048, m <= 512: C3 / C4)
+#define UPD_THREADS 256   // small-branch limits P <= UPD_CAP x 256 = 2048, m <= 512 (C3 / C4); k_fused_const
+#define UPD_THREADS_S 512  // the small-branch update kernel
 #define UPD_THREADS_L 1024  // large branches (C2: P = 8028, m = 2000; wide / generic)
 
 // Recompute the fused-path constants of branch b from theta: per column k of
@@ -502,17 +503,15 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
   }
 }
 
-// small: branches with P <= 2048 and m <= 512 (256 threads; 512 when the launch has at most
-// one branch per CU: N = 8 shard 0.0163 -> 0.0129 ms); large: the rest (1024 threads)
+// small: branches with P <= 2048 and m <= 512 (512 threads: more loads in flight per branch
+// than 256, N = 8 shard 0.0163 -> 0.0129 ms, C3 unchanged); large: the rest (1024 threads)
 void launch_update(const DevState& st, const int32_t* branches, int32_t nb, int32_t mode, int32_t step,
                    hipStream_t s, int large) {
   if (nb <= 0) return;
   if (large)
     hipLaunchKernelGGL((k_update<UPD_THREADS_L, 4>), dim3(nb), dim3(UPD_THREADS_L), 0, s, st, branches, mode, step);
-  else if (nb <= 256)  // at most one workgroup per CU: 512 threads, more loads in flight per branch
-    hipLaunchKernelGGL((k_update<512, 1>), dim3(nb), dim3(512), 0, s, st, branches, mode, step);
-  else
-    hipLaunchKernelGGL((k_update<UPD_THREADS, 2>), dim3(nb), dim3(UPD_THREADS), 0, s, st, branches, mode, step);
+  else  // one block size for every launch: the reductions' order, hence every bit, does not depend on nb
+    hipLaunchKernelGGL((k_update<UPD_THREADS_S, 1>), dim3(nb), dim3(UPD_THREADS_S), 0, s, st, branches, mode, step);
 }
 
 bool update_is_large(const BranchDev& d) { return d.P > UPD_CAP * UPD_THREADS || d.m > 2 * UPD_THREADS; }
