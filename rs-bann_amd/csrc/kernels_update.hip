@@ -142,8 +142,8 @@ __device__ void block_sum_n(double (&v)[NV], double* red) {
   }
 }
 
-// Register-resident update of a small fused branch (P <= UPD_CAP * 256, m <= 512,
-// <= 4 first-layer columns: every C2/C3/C4 branch).  All global loads of the
+// Register-resident update of a fused branch (P <= UPD_CAP * NT, m <= MPT * NT, <= 4
+// first-layer columns, or a wide branch with <= 32: every C2/C3/C4/C5 branch).  All global loads of the
 // step are issued up front (partials, theta, lambda, momentum, eps, theta0,
 // mu, sigma), the parameters stay in registers between the reduction and the
 // position step, and the W0-digit refresh reads the new W0 from LDS: two
@@ -284,82 +284,90 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     s_th[i] = tn;
   }
   __syncthreads();
-  // ---- W0 digit refresh from the new W0 in LDS (the general refresh_fused_const) ----
+  // ---- W0 digit refresh from the new W0 in LDS (the general refresh_fused_const),
+  // four columns per pass (wide branches: eight passes, digit image of 8 column blocks) ----
   const float* W0 = s_th + bd.woff[0];
   const float* b0 = s_th + bd.boff[0];
-  float mx[4] = {0.f, 0.f, 0.f, 0.f};
-  double cs[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int c = 0; c < MPT; ++c) {
-    const int j = t + c * NT;
-    if (j >= m) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (q < w0) {
-        const float wp = sgs[c] > 0.f ? W0[q * m + j] / sgs[c] : 0.f;
-        mx[q] = fmaxf(mx[q], fabsf(wp));
-        cs[q] += (double)mus[c] * (double)wp;
-      }
-  }
+  const int NB = bd.fused == 2 ? 8 : 1;
+  uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
   __shared__ float s_mx[4][NT / 64];
   __shared__ double s_cs[4][NT / 64];
   const int wv = t >> 6;
+  for (int k0 = 0; k0 < w0; k0 += 4) {
+    const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    double cs[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+    for (int c = 0; c < MPT; ++c) {
+      const int j = t + c * NT;
+      if (j >= m) continue;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
-      cs[q] += __shfl_xor(cs[q], o);
+      for (int q = 0; q < 4; ++q)
+        if (q < nk) {
+          const float wp = sgs[c] > 0.f ? W0[(k0 + q) * m + j] / sgs[c] : 0.f;
+          mx[q] = fmaxf(mx[q], fabsf(wp));
+          cs[q] += (double)mus[c] * (double)wp;
+        }
     }
-  if ((t & 63) == 0)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s_mx[q][wv] = mx[q];
-      s_cs[q][wv] = cs[q];
-    }
-  __syncthreads();
-  double inv[4];
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float M = s_mx[q][0];
-    double C = s_cs[q][0];
-    for (int w = 1; w < NT / 64; ++w) {
-      M = fmaxf(M, s_mx[q][w]);
-      C += s_cs[q][w];
-    }
-    float sc = 1.f;  // s = 2^e with max/s <= 127
-    if (M > 0.f) {
-      int e;
-      frexpf(M / 127.f, &e);
-      sc = ldexpf(1.f, e);
-    }
-    inv[q] = 1.0 / (double)sc;
-    if (t == 0 && q < w0) {
-      st.fc[b].scale[q] = sc;
-      st.fc[b].c0[q] = (float)((double)b0[q] - C);
-    }
-  }
-  uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
-#pragma unroll
-  for (int c = 0; c < MPT; ++c) {
-    const int j = t + c * NT;
-    if (j >= m) continue;
-    const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (q >= w0) continue;
-      const float wp = sgs[c] > 0.f ? W0[q * m + j] / sgs[c] : 0.f;
-      double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
-      int8_t dq[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const double r = rint(v);
-        dq[d] = (int8_t)r;
-        v = (v - r) * 128.0;
+      for (int o = 32; o > 0; o >>= 1) {
+        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
+        cs[q] += __shfl_xor(cs[q], o);
       }
+    if ((t & 63) == 0)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) dig[(((int64_t)ch * 64 + 16 * grp + 4 * q + d) * 16) + jj] = (uint8_t)dq[d];
+      for (int q = 0; q < 4; ++q) {
+        s_mx[q][wv] = mx[q];
+        s_cs[q][wv] = cs[q];
+      }
+    __syncthreads();
+    double inv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float M = s_mx[q][0];
+      double C = s_cs[q][0];
+      for (int w = 1; w < NT / 64; ++w) {
+        M = fmaxf(M, s_mx[q][w]);
+        C += s_cs[q][w];
+      }
+      float sc = 1.f;  // s = 2^e with max/s <= 127
+      if (M > 0.f) {
+        int e;
+        frexpf(M / 127.f, &e);
+        sc = ldexpf(1.f, e);
+      }
+      inv[q] = 1.0 / (double)sc;
+      if (t == 0 && q < nk) {
+        st.fc[b].scale[k0 + q] = sc;
+        st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
+      }
     }
+#pragma unroll
+    for (int c = 0; c < MPT; ++c) {
+      const int j = t + c * NT;
+      if (j >= m) continue;
+      const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q >= nk) continue;
+        const int k = k0 + q;
+        const float wp = sgs[c] > 0.f ? W0[k * m + j] / sgs[c] : 0.f;
+        double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
+        int8_t dq[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const double r = rint(v);
+          dq[d] = (int8_t)r;
+          v = (v - r) * 128.0;
+        }
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          dig[((((int64_t)ch * NB + (k >> 2)) * 64 + 16 * grp + 4 * (k & 3) + d) * 16) + jj] = (uint8_t)dq[d];
+      }
+    }
+    if (k0 + 4 < w0) __syncthreads();  // s_mx / s_cs are rewritten by the next pass
   }
 }
 
@@ -387,7 +395,8 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
     }
     return;
   }
-  if ((bd.fused == 1 || bd.fused == 3) && P <= UPD_CAP * NT && bd.m <= MPT * NT && bd.widths[0] <= 4) {
+  if ((((bd.fused == 1 || bd.fused == 3) && bd.widths[0] <= 4) || (bd.fused == 2 && bd.widths[0] <= 32)) &&
+      P <= UPD_CAP * NT && bd.m <= MPT * NT) {
     __shared__ float s_th[UPD_CAP * NT];
     update_small<NT, MPT>(st, b, bd, mode, prof, step, redd, s_th);  // checks the status itself
     return;
