@@ -43,6 +43,9 @@
 #include "bann_internal.h"
 #include "kernel_util.h"
 
+#ifndef GX_ABL
+#define GX_ABL 0
+#endif
 #define GX_T 64                // output tile edge, K block depth
 #define GX_PREP_Y 16           // k_gx_prep workgroups per branch
 #define GX_LD 68               // LDS row stride (floats)
@@ -907,16 +910,24 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
     for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
   }
   auto load = [&](int64_t kb) {
+#if !(GX_ABL & 2)
     blk2_load<ARK>(ra, Am, lda, bnd_a(kb));
+#endif
+#if !(GX_ABL & 1)
     if constexpr (BP) load_bp(rbp, kb);
     else blk2_load<BRK>(rb, Bm, ldb, bnd_b(kb));
+#endif
   };
   if (kb0 < kb1) load(kb0);
   for (int64_t kb = kb0; kb < kb1; ++kb) {
+#if !(GX_ABL & 2)  // profiling builds: GX_ABL 1 / 2 skip the B / A staging, 4 the MFMAs
     blk2_store<ARK, false>(ra, bnd_a(kb), As, csa);
+#endif
+#if !(GX_ABL & 1)
     if constexpr (BP) store_bp(rbp);
     else if (want_cs) blk2_store<BRK, true>(rb, bnd_b(kb), Bs, csp);
     else blk2_store<BRK, false>(rb, bnd_b(kb), Bs, csp);
+#endif
     __syncthreads();
     if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
     bf16x8 a[2][3];
@@ -932,6 +943,10 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
 #pragma unroll
       for (int X = 0; X < 2; ++X) {
         v4f& c = acc[2 * X + Y];
+#if GX_ABL & 4
+        c += v4f{(float)a[X][2][0], (float)bq[0][1], (float)a[X][0][3], (float)bq[2][5]};
+        continue;
+#endif
         // small products first
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][2], bq[0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][1], bq[1], c, 0, 0, 0);
