@@ -797,16 +797,21 @@ __device__ __forceinline__ bf16x8 frag3(const __bf16* P, int pl, int rb, int li,
 }
 }  // namespace
 
+#if GX_ABL & 8  // profiling build: two LDS stages (one barrier per K block, 2 workgroups per CU)
+#define GX_X3_NB 2
+#else
+#define GX_X3_NB 1
+#endif
 template <int PH>
-__global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
+__global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 4))
     k_gx_gemm_x3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
                  int total, int per) {
   constexpr bool ARK = PH != GX_GRAD;  // A staged [row][k]
   constexpr bool BRK = PH == GX_FWD;   // B staged [row][k]
   constexpr bool F64 = PH == GX_GRAD;
-  __shared__ __attribute__((aligned(16))) __bf16 As[3 * GX_PL];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * GX_PL];
-  __shared__ double cs_s[16][GX_T];
+  __shared__ __attribute__((aligned(16))) __bf16 As_[GX_X3_NB][3 * GX_PL];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs_[GX_X3_NB][3 * GX_PL];
+  __shared__ double cs_s[PH == GX_GRAD ? 16 : 1][GX_T];  // GRAD's column sums only
   const int q = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD-aware numbering (k_gx_gemm)
   if (q >= total) return;
   int lo_ = 0, hi_ = nb;
@@ -894,7 +899,7 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
     for (int pl = 0; pl < 3; ++pl)
       rp_[pl] = ok ? *reinterpret_cast<const v4i*>(Wp3 + pl * p3 + row * l3 + col) : v4i{0, 0, 0, 0};
   };
-  auto store_bp = [&](v4i (&rp_)[3]) {
+  auto store_bp = [&](v4i (&rp_)[3], __bf16* Bs) {
     const int off = PH == GX_FWD ? (t >> 2) * GX_RK + 8 * (t & 3) : (t >> 3) * GX_KR + 8 * (t & 7);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<v4i*>(&Bs[pl * GX_PL + off]) = rp_[pl];
@@ -918,18 +923,21 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
     else blk2_load<BRK>(rb, Bm, ldb, bnd_b(kb));
 #endif
   };
-  if (kb0 < kb1) load(kb0);
-  for (int64_t kb = kb0; kb < kb1; ++kb) {
+  auto stage = [&](int64_t kb, int buf) {
+    __bf16* As = As_[buf];
+    __bf16* Bs = Bs_[buf];
 #if !(GX_ABL & 2)  // profiling builds: GX_ABL 1 / 2 skip the B / A staging, 4 the MFMAs
     blk2_store<ARK, false>(ra, bnd_a(kb), As, csa);
 #endif
 #if !(GX_ABL & 1)
-    if constexpr (BP) store_bp(rbp);
+    if constexpr (BP) store_bp(rbp, Bs);
     else if (want_cs) blk2_store<BRK, true>(rb, bnd_b(kb), Bs, csp);
     else blk2_store<BRK, false>(rb, bnd_b(kb), Bs, csp);
 #endif
-    __syncthreads();
-    if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
+  };
+  auto compute = [&](int64_t kb, int buf) {
+    const __bf16* As = As_[buf];
+    const __bf16* Bs = Bs_[buf];
     bf16x8 a[2][3];
 #pragma unroll
     for (int X = 0; X < 2; ++X)
@@ -968,7 +976,31 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD ? 3 : 4)
         }
       }
     }
-    __syncthreads();  // every wave is done with the stage before it is refilled
+  };
+  if (kb0 < kb1) load(kb0);
+  if constexpr (GX_X3_NB == 1) {
+    for (int64_t kb = kb0; kb < kb1; ++kb) {
+      stage(kb, 0);
+      __syncthreads();
+      if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
+      compute(kb, 0);
+      __syncthreads();  // every wave is done with the stage before it is refilled
+    }
+  } else {  // stage kb + 1 into the other buffer while kb computes: one barrier per block
+    if (kb0 < kb1) {
+      stage(kb0, 0);
+      if (kb0 + 1 < kb1) load(kb0 + 1);
+      __syncthreads();
+    }
+    for (int64_t kb = kb0; kb < kb1; ++kb) {
+      const int buf = (int)((kb - kb0) & 1);
+      compute(kb, buf);
+      if (kb + 1 < kb1) {
+        stage(kb + 1, buf ^ 1);
+        if (kb + 2 < kb1) load(kb + 2);
+      }
+      __syncthreads();
+    }
   }
   if constexpr (F64) {  // an odd block count leaves one block in acc
 #pragma unroll
