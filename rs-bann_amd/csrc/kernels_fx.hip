@@ -47,6 +47,18 @@
 #define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
 #define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
 #define FX_DROW 256       // delta0 digit image: 16 rows x 16 B per K group (read twice per tile)
+// FX_DEEP: the stream runs TWO tiles ahead in the same two slots -- chunk c of
+// tile t + 2 is issued into tile t's slot as soon as tile t's backward has read
+// chunk c's last window (the target piece once the head has read the target),
+// so a piece has a whole tile more to land than when it is issued in the forward
+// (profiling build ABL=524288: the one-tile-ahead stream, issued in the forward)
+#ifndef FX_DEEP
+#if BANN_ABLATE & 524288
+#define FX_DEEP 0
+#else
+#define FX_DEEP 1
+#endif
+#endif
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -277,9 +289,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   if (tt < te) {
     for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
+    if (FX_DEEP && tt + NW < te) {
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
+      issue_y(tt + NW, 1);
+    }
   }
   for (; tt < te; tt += NW, sl ^= 1) {
     const bool more = tt + NW < te;
+    const bool more2 = FX_DEEP && tt + 2 * NW < te;  // deep stream: tile tt + 2 NW goes into this slot
     FX_STAMP(0);
     // tile tt (issued during tile tt - NW) has landed.  (An L2 prefetch of the
     // tile after it measured +3 %: with 8 waves/CU the L2 is already the DMA's
@@ -287,7 +304,13 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 #if BANN_ABLATE & 2048
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(ynx)::"memory");
 #else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (FX_DEEP) {
+      // the nch + 1 pieces of tile tt + NW are younger (loads return in order; a
+      // younger pred store still outstanding only makes this wait longer)
+      vm_wait(more ? nch + 1 : 0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #endif
     FX_STAMP(1);
     const char* xs = &s_x[wave][sl][0];
@@ -333,7 +356,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
           Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
         }
-        if (more) issue_chunk(tt + NW, sl ^ 1, c);
+        if (!FX_DEEP && more) issue_chunk(tt + NW, sl ^ 1, c);
         // fragment q = field q of every byte, kept in place (x 4^q, folded into the
         // digit combine below) except q = 3 (bits 6-7 would overflow int8)
         const v4i B0 = (v4i)(Xc & 0x03030303u);
@@ -380,7 +403,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 #else
     const float yv = s_y[wave][sl][lane];
 #endif
-    if (more) issue_y(tt + NW, sl ^ 1);
+    if (!FX_DEEP && more) issue_y(tt + NW, sl ^ 1);
     float d[4];
 #if BANN_ABLATE & 1
     d[0] = z0 * 1e-3f - yv;
@@ -469,6 +492,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       }
     }
 
+    if (more2) {  // the target has been read (yv in a register): its slot takes tile tt + 2 NW's
+      asm volatile("" ::"v"(yv));
+      issue_y(tt + 2 * NW, sl);
+    }
     __builtin_amdgcn_sched_barrier(0);
     FX_STAMP(3);
     // the backward's first genotype windows: their LDS reads fly under the digit phase
@@ -557,6 +584,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         const v4i Bv = Bn;
         Bn = Bn2;
         if (u + 2 < 32 && (NCH != 0 || u + 2 < 4 * nch)) Bn2 = unpack(wq[(u + 2) % PD]);
+        if (more2 && (u & 3) == 1) {  // window 4c + 3, chunk c's last, is unpacked: refill chunk c
+          asm volatile("" ::"v"(Bn2[0]), "v"(Bn2[1]), "v"(Bn2[2]), "v"(Bn2[3]));
+          issue_chunk(tt + 2 * NW, sl, u >> 2);
+        }
         if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))  // slot of window u, consumed two iterations ago
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
 #endif
