@@ -19,7 +19,7 @@
 //     digit carry in the rare case a tile's |delta0| outgrows it), converted to
 //     f32 once at the end;
 //   * waves never wait for each other inside the tile loop: each streams its
-//     own tiles into its own LDS slots (LDS-DMA, one tile ahead, counted
+//     own tiles into its own LDS slots (LDS-DMA, two tiles ahead, counted
 //     vmcnt) -- the only barriers are the final workgroup reduction.
 //
 // Genotype tile image (HBM == LDS, 16 B per marker row, "u2t" layout):
