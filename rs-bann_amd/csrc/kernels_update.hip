@@ -293,6 +293,70 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   __shared__ float s_mx[4][NT / 64];
   __shared__ double s_cs[4][NT / 64];
   const int wv = t >> 6;
+  if (NT == 1024 && NB == 8 && m <= 128) {
+    // wide branches (C5: m = 125, w0 = 32): the eight four-column passes run side by
+    // side -- thread t takes marker t & 127 of column quad t >> 7 (waves 2q, 2q + 1),
+    // one barrier instead of sixteen.  The lane -> marker map and the reduction order
+    // are those of the pass loop below, so every bit of the digits, scales and c0 is too.
+    const int j = t & 127, kq = t >> 7;
+    const bool on = j < m;
+    const float sg = on ? st.sigma[bd.mk_off + j] : 0.f;
+    const float mu = on ? st.mu[bd.mk_off + j] : 0.f;
+    float mx[4], wq[4];
+    double cs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = 4 * kq + q;
+      wq[q] = (on && k < w0 && sg > 0.f) ? W0[k * m + j] / sg : 0.f;
+      mx[q] = fmaxf(0.f, fabsf(wq[q]));
+      cs[q] = 0.0;
+      if (on && k < w0) cs[q] += (double)mu * (double)wq[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
+        cs[q] += __shfl_xor(cs[q], o);
+      }
+    __shared__ float s_mx8[NT / 64][4];
+    __shared__ double s_cs8[NT / 64][4];
+    if ((t & 63) == 0)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s_mx8[wv][q] = mx[q];
+        s_cs8[wv][q] = cs[q];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = 4 * kq + q;
+      // (+ the other waves' zeros, as the pass loop adds them)
+      const float M = fmaxf(fmaxf(s_mx8[2 * kq][q], s_mx8[2 * kq + 1][q]), 0.f);
+      const double C = (s_cs8[2 * kq][q] + s_cs8[2 * kq + 1][q]) + 0.0;
+      float sc = 1.f;  // s = 2^e with max/s <= 127
+      if (M > 0.f) {
+        int e;
+        frexpf(M / 127.f, &e);
+        sc = ldexpf(1.f, e);
+      }
+      if (j == 0 && k < w0) {
+        st.fc[b].scale[k] = sc;
+        st.fc[b].c0[k] = (float)((double)b0[k] - C);
+      }
+      if (on && k < w0) {
+        double v = (double)wq[q] * (1.0 / (double)sc);
+        const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const double r = rint(v);
+          dig[((((int64_t)ch * NB + kq) * 64 + 16 * grp + 4 * q + d) * 16) + jj] = (uint8_t)(int8_t)r;
+          v = (v - r) * 128.0;
+        }
+      }
+    }
+    return;
+  }
   for (int k0 = 0; k0 < w0; k0 += 4) {
     const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
     float mx[4] = {0.f, 0.f, 0.f, 0.f};
