@@ -51,7 +51,13 @@
 // tile t + 2 is issued into tile t's slot as soon as tile t's backward has read
 // chunk c's last window (the target piece once the head has read the target),
 // so a piece has a whole tile more to land than when it is issued in the forward
-// (profiling build ABL=524288: the one-tile-ahead stream, issued in the forward)
+// (profiling build ABL=524288: the one-tile-ahead stream, issued in the forward;
+// ABL=1048576: the deep stream's pieces issued after the backward in one burst)
+#if BANN_ABLATE & 1048576
+#define FX_SPREAD 0
+#else
+#define FX_SPREAD 1
+#endif
 #ifndef FX_DEEP
 #if BANN_ABLATE & 524288
 #define FX_DEEP 0
@@ -327,7 +333,11 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // (software pipelined: the LDS reads of chunk c + 1 fly while chunk c's
     // four MFMAs issue; sched barriers keep the compiler from hoisting more)
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
-#if BANN_ABLATE & 4096
+    // the forward at raised priority too (with the stream issued in the backward:
+    // -1.2 % per launch, A/B tools/gpu_ab.sh; profiling build ABL=4096: priority 0)
+#if BANN_ABLATE & 4194304
+    __builtin_amdgcn_s_setprio(2);  // profiling build: the forward above the head
+#elif !(BANN_ABLATE & 4096)
     __builtin_amdgcn_s_setprio(1);
 #endif
     {
@@ -378,13 +388,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-#if BANN_ABLATE & 4096
-    __builtin_amdgcn_s_setprio(0);
-#endif
     // the head + digit phase is a dependent VALU chain: at raised priority it
     // takes the SIMD's issue slots ahead of the partner wave's independent
     // MFMA/unpack stream (measured -1 %)
+#if BANN_ABLATE & 2097152
+    __builtin_amdgcn_s_setprio(2);  // profiling build: the head above the forward
+#else
     __builtin_amdgcn_s_setprio(1);
+#endif
     FX_STAMP(2);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
@@ -584,7 +595,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         const v4i Bv = Bn;
         Bn = Bn2;
         if (u + 2 < 32 && (NCH != 0 || u + 2 < 4 * nch)) Bn2 = unpack(wq[(u + 2) % PD]);
-        if (more2 && (u & 3) == 1) {  // window 4c + 3, chunk c's last, is unpacked: refill chunk c
+        if (FX_SPREAD && more2 && (u & 3) == 1) {  // window 4c + 3, chunk c's last, is unpacked: refill chunk c
           asm volatile("" ::"v"(Bn2[0]), "v"(Bn2[1]), "v"(Bn2[2]), "v"(Bn2[3]));
           issue_chunk(tt + 2 * NW, sl, u >> 2);
         }
@@ -599,6 +610,13 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+#if BANN_ABLATE & 1048576
+    // profiling build: tile tt + 2 NW's pieces issued after the backward, in one burst
+    if (more2) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + 2 * NW, sl, c);
+    }
+#endif
     FX_STAMP(5);
 #if BANN_ABLATE & 16
     ++ntl;
