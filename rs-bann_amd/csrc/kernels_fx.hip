@@ -940,6 +940,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 
     // ---- forward: partial Z0 over this wave's block ----
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+#if BANN_ABLATE & 8388608
+    __builtin_amdgcn_s_setprio(1);  // profiling build: the forward at raised priority (as fx)
+#endif
     {
       v4i Dg[8];
       Dg[0] = Dn0;

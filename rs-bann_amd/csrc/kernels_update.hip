@@ -151,6 +151,10 @@ __device__ void block_sum_n(double (&v)[NV], double* red) {
 // seven dependent global round trips (the launch follows a genotype stream that
 // has evicted all of it from L2).  Same arithmetic as the general path below.
 #define UPD_CAP 8
+// parameters per thread: the 512-thread kernel only takes P <= 2048 (update_is_large
+// sends the rest to the 1024-thread one), so 4 -- 20 fewer VGPRs, same bits
+template <int NT>
+constexpr int upd_cap() { return NT == 512 ? 4 : UPD_CAP; }
 template <int NT, int MPT>
 __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int mode, bool prof, int step,
                              double* redd, float* s_th) {
@@ -173,10 +177,11 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
   const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
   const bool lasso = (bd.prior == 2 || bd.prior == 3);
-  float th[UPD_CAP], gr[UPD_CAP], pm[UPD_CAP], ep[UPD_CAP], t0[UPD_CAP];
+  constexpr int CAP = upd_cap<NT>();
+  float th[CAP], gr[CAP], pm[CAP], ep[CAP], t0[CAP];
   double sums[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-  for (int c = 0; c < UPD_CAP; ++c) {
+  for (int c = 0; c < CAP; ++c) {
     const int i = t + c * NT;
     th[c] = gr[c] = pm[c] = ep[c] = t0[c] = 0.f;
     if (i >= P) continue;
@@ -203,7 +208,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
   if (check && status != ST_RUNNING) return;
   if (!prof)
 #pragma unroll
-    for (int c = 0; c < UPD_CAP; ++c)
+    for (int c = 0; c < CAP; ++c)
       if (t + c * NT < P) st.grad[base + t + c * NT] = gr[c];
   if (mode == MODE_GRAD) {
     double v1[1] = {sums[0]};
@@ -259,7 +264,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     }
   }
 #pragma unroll
-  for (int c = 0; c < UPD_CAP; ++c) {
+  for (int c = 0; c < CAP; ++c) {
     const int i = t + c * NT;
     if (i >= P) continue;
     float tn = th[c];
@@ -443,7 +448,11 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
 // 18 % of a step at 125 branches per GPU.)  MODE_PROFILE repeats STEP's work
 // without changing the chain (bann_profile_session).
 template <int NT, int MPT>
-__global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __restrict__ blist, int mode, int step) {
+#ifndef UPD_WPE
+#define UPD_WPE 8  // A/B builds: -DUPD_WPE=1 leaves the register budget to the compiler
+#endif
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? UPD_WPE : 1)))  // 512: <= 64 VGPRs, four per CU (C3: 1000 in one round)
+    k_update(DevState st, const int32_t* __restrict__ blist, int mode, int step) {
   __shared__ double redd[4 * (NT / 64)];
   const int b = blist[blockIdx.x];
   const BranchDev bd = st.br[b];
@@ -460,8 +469,8 @@ __global__ void __launch_bounds__(NT) k_update(DevState st, const int32_t* __res
     return;
   }
   if ((((bd.fused == 1 || bd.fused == 3) && bd.widths[0] <= 4) || (bd.fused == 2 && bd.widths[0] <= 32)) &&
-      P <= UPD_CAP * NT && bd.m <= MPT * NT) {
-    __shared__ float s_th[UPD_CAP * NT];
+      P <= upd_cap<NT>() * NT && bd.m <= MPT * NT) {
+    __shared__ float s_th[upd_cap<NT>() * NT];
     update_small<NT, MPT>(st, b, bd, mode, prof, step, redd, s_th);  // checks the status itself
     return;
   }
