@@ -12,9 +12,13 @@ steps.  Genotypes are synthetic (generated on the device), resident in HBM as
 int8 before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W]
-  (N > 1: launched by torch.distributed.run, one rank per GPU; the 1k branches
-   are sharded over the ranks, no collective inside a step; the trajectory end
-   all-reduces the n-vector residual change over RCCL.)
+  (N > 1: one rank per GPU.  Run directly, bench.py starts the N ranks itself
+   -- torch.distributed.run as a CHILD process, before anything touches the GPU
+   -- and rank 0's JSON line passes through; under an outer
+   torch.distributed.run (WORLD_SIZE set) it is one of the ranks.  The 1k
+   branches are sharded over the ranks, no collective inside a step; the
+   trajectory end all-reduces the n-vector residual change over RCCL.
+   BANN_DIST_BACKEND=gloo rehearses N ranks on one GPU.)
 
 Prints ONE JSON line (rank 0).
 """
@@ -89,6 +93,54 @@ def cpu_baseline(n, m, widths, sample_branches, sample_steps):
     return dict(branch_steps_per_s=branch_steps_per_s, threads=threads, seconds=t, setup_s=setup.value)
 
 
+def launch_ranks(nproc: int) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start the N ranks as
+    `torch.distributed.run` in a child process -- never exec, and nothing here
+    touches the GPU -- wait for it and return its exit code.  The ranks inherit
+    stdout, so rank 0's JSON line is this command's output."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only (RCCL across processes)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"bench.py: launching {nproc} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
+
+
+def check_launch(dist, world, rank, n=4096, nbranches=1000):
+    """--check-launch: the multi-rank plumbing without a GPU (CPU test): every
+    rank takes its marker-balanced branch shard (bann_shard_branches) and runs
+    the library's residual exchange step (bann_residual_update_host: the sum
+    over ranks of the local residual changes through the communicator's
+    all-reduce, then residual -= sum -- what bann_exchange_residual does for a
+    callback communicator) on a rank-specific change; rank 0 prints one JSON line."""
+    import torch
+    from bann.distributed import TorchAllreduce, residual_update, shard_ranges
+    lo, hi = shard_ranges([500] * nbranches, world)[rank]
+    base = np.linspace(-1.0, 1.0, n, dtype=np.float32)
+    delta = (np.arange(n, dtype=np.float32) % 7) * np.float32(rank + 1)   # this rank's local change
+    res = residual_update(base.copy(), delta, TorchAllreduce(dist) if dist is not None else None)
+    want = base - (np.arange(n, dtype=np.float32) % 7) * np.float32(world * (world + 1) / 2)
+    rec = torch.tensor([rank, lo, hi, float(np.max(np.abs(res - want)))], dtype=torch.float64)
+    if dist is not None:
+        recs = [torch.zeros_like(rec) for _ in range(world)]
+        dist.all_gather(recs, rec)
+    else:
+        recs = [rec]
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "n_gpus": world,
+                          "ranks": [int(r[0]) for r in recs],
+                          "shards": [[int(r[1]), int(r[2])] for r in recs],
+                          "exchange_max_err": max(float(r[3]) for r in recs),
+                          "parallelism": f"branch-shard x{world}"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,7 +152,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-branches", type=int, default=None)   # default 96 (c3def: 4), capped at the branch count
     ap.add_argument("--cpu-sample-steps", type=int, default=None)      # default 16 (c3def: 2)
-    ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--profile-iters", type=int, default=20)
+    ap.add_argument("--no-launch-timing", action="store_true",
+                    help="no HIP events around the timed trajectory's launches (roofline from the back-to-back session)")
     ap.add_argument("--emulate-shard", type=int, default=0,
                     help="profiling only: run rank 0's shard of an N-GPU job on this one GPU, no collective")
     ap.add_argument("--hidden-bf16", action="store_true",
@@ -111,21 +165,31 @@ def main():
                          "branch outputs all-reduced every leapfrog step (bann_network_hmc_step); sequential: the "
                          "reference's own sweep order, one branch at a time against the refreshed residual "
                          "(bann_net_train, Net::train net.rs:201-358), one GPU")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="no GPU: run the N-rank launch, shard and the library's residual exchange step only (CPU test)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    backend = os.environ.get("BANN_DIST_BACKEND", "nccl")   # gloo: rehearse N ranks on one GPU
+    backend = os.environ.get("BANN_DIST_BACKEND", "gloo" if args.check_launch else "nccl")   # gloo: N ranks on one GPU
     dist_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch
         import torch.distributed as dist_mod
-        local_rank = local_rank % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local_rank)
+        if not args.check_launch:
+            local_rank = local_rank % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local_rank)
         dist_mod.init_process_group(backend, init_method="env://")
         dist = dist_mod
+    if args.check_launch:
+        check_launch(dist, world, rank)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from bann import BannContext
     from bann.distributed import TorchAllreduce, comm_unique_id, shard_ranges
@@ -192,8 +256,10 @@ def main():
         prec = precs[k]
         prec[len(widths) - 1] = np.array([out_prec])
         ctx.set_precisions(k, np.concatenate(prec).astype(np.float32))
-    for k in range(nb):
-        ctx.set_target(k, (noise + preds[k]).astype(np.float32))
+    # the sweep's residual y - sum_b f_b (net.rs:279-300) lives on the device; every
+    # branch target y_b = residual + f_b is built there in one launch
+    ctx.residual_set(noise.astype(np.float32))
+    ctx.rebuild_targets(list(range(nb)))
     del preds
     ctx.synchronize()
     setup_s = time.time() - t_setup
@@ -212,7 +278,6 @@ def main():
             ctx.comm_callback(TorchAllreduce(dist), world, rank)
         torch.cuda.synchronize()
     branches = list(range(nb))
-    residual = noise.astype(np.float32)   # the sweep's residual y - sum_b f_b (net.rs:279-300)
     y_net = (noise + fsum).astype(np.float32)
 
     net, seen = None, [0.0]
@@ -226,29 +291,47 @@ def main():
     def trajectory(L, seed):
         """one HMC trajectory of L leapfrog steps.  branch sampler: every branch of
         this rank (momentum draw + initial gradient, L fused steps, Metropolis),
-        then the residual change of the accepted branches exchanged over the ranks
-        inside the library (bann_exchange_residual).  network sampler: one HMC
-        state over all branches of all ranks, the summed outputs all-reduced every
-        step (bann_network_hmc_step)."""
-        nonlocal residual
+        then the residual change of the accepted branches summed over the ranks into
+        the device residual (bann_exchange_residual_device) and every branch target
+        rebuilt from it for the next trajectory (bann_rebuild_targets).  network
+        sampler: one HMC state over all branches of all ranks, the summed outputs
+        all-reduced every step (bann_network_hmc_step)."""
         if args.sampler == "sequential":   # one sweep: every branch one L-step trajectory, in shuffled order
             net.train(y_net, MCMCConfig(hmc_step_size_factor=args.step_factor, hmc_integration_length=L,
                                         chain_length=1, burn_in=1))
             before, seen[0] = seen[0], float(net.summary()["num_accepted"])
             return seen[0] - before
         if args.sampler == "network":
+            # the Metropolis uniform: drawn by the library on rank 0 (seed) and shared
             r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov",
-                                     step_factor=args.step_factor, seed=seed, u=0.5)
+                                     step_factor=args.step_factor, seed=seed)
             return float(r["status"] == 0) * nb
         ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
         ctx.leapfrog_steps(L)
         status, acc = ctx.leapfrog_end()
-        residual = ctx.exchange_residual(residual)
+        ctx.exchange_residual_device()
+        ctx.rebuild_targets(branches)
         return acc
 
-    # warmup: a full trajectory of W steps (loads every kernel, ramps the clocks)
+    # warmup: a full trajectory of W steps (loads every kernel), then the
+    # roofline's back-to-back launch timing (bann_profile_session: a 2-step
+    # trajectory whose gradient and update launches are repeated profile_iters
+    # times without changing the chain) -- untimed work that also lets the GPU's
+    # clock settle under the HBM load before the timed trajectory (the first
+    # ~10 gradient launches after a light phase run up to 30 % slow while the
+    # power controller settles: profiles/r03a_transient.md)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
+    ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99 + rank)
+    b2b_grad_ms, b2b_upd_ms = ctx.profile_session(args.profile_iters)
+    ctx.leapfrog_end()
+    if args.sampler == "branch":
+        ctx.exchange_residual_device()
+        ctx.rebuild_targets(branches)
+    timing = args.sampler == "branch" and not args.no_launch_timing
+    if timing:   # HIP events around every gradient / update launch of the timed trajectory
+        ctx.launch_timing(reset=True)
+        ctx.set_launch_timing(True)
     ctx.synchronize()
     if dist is not None:
         torch.cuda.synchronize()
@@ -260,6 +343,11 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if timing:
+        ctx.set_launch_timing(False)
+        grad_ms, upd_ms, n_launch = ctx.launch_timing(reset=True)
+    else:
+        grad_ms, upd_ms, n_launch = b2b_grad_ms, b2b_upd_ms, 0
     if dist is not None:
         te = torch.tensor([elapsed], device=dist_dev, dtype=torch.float64)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
@@ -276,10 +364,9 @@ def main():
                 (", sequential Net::train sweep (one branch at a time)" if args.sampler == "sequential" else ""))
     kernel_name = {"wide": "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
                    "layered": "k_gx_gemm"}[path]
-    # ---- kernel timing for the roofline (HIP events on the library stream) ----
-    ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99)
-    grad_ms, upd_ms = ctx.profile_session(args.profile_iters)
-    ctx.leapfrog_end()
+    # ---- kernel timing for the roofline: HIP events on the library stream around
+    # the timed trajectory's own gradient launches (bann_set_launch_timing); the
+    # back-to-back figure of the warmup session is reported beside it ----
     # algorithmic bytes per gradient launch: the genotype block of every branch
     # read once at its information content -- 2 bits per genotype, i.e. the
     # .bed payload size ceil(n/4) * m_b (bed.rs:193-245) -- plus the per-branch
@@ -358,7 +445,10 @@ def main():
                          {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": achieved / HBM_PEAK_GBS}) | {"traffic": traffic,
                          "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
-                         "kernel": kernel_name, "kernel_ms": grad_ms, "alg_bytes_per_launch": alg_bytes,
+                         "kernel": kernel_name, "kernel_ms": grad_ms,
+                         "kernel_ms_source": (f"HIP events around the {n_launch} gradient launches of the timed "
+                                              "trajectory" if n_launch else "back-to-back launches (bann_profile_session)"),
+                         "kernel_ms_back_to_back": b2b_grad_ms, "alg_bytes_per_launch": alg_bytes,
                          "packed_bytes_per_launch": ctx.packed_genotype_bytes,
                          "alg_bytes_basis": "2-bit genotypes (n*m_b/4) + 4n target bytes per branch", "update_kernel_ms": upd_ms},
             "cpu_baseline": cpu,

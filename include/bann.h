@@ -72,9 +72,11 @@ const char* bann_version(void);
 
 /* ---------------- genotypes: replaces GroupedGenotypes / BedVM ----------------
  * genotypes.rs:7-12,44-48 (x_group_af), bed.rs:193-245 (from_file + column
- * stats), bed.rs:325-355 (get_submatrix_af_standardized).  The matrix stays
- * resident on the device as int8 genotypes; standardization (g - mu)/sigma
- * with the population std (bed.rs:231-242) is folded into the kernels. */
+ * stats), bed.rs:325-355 (get_submatrix_af_standardized).  The cohort stays
+ * resident on the device as a 2-bit variant-major image (the .bed payload's
+ * information content), packed at bann_finalize into per-branch 2-bit tile
+ * images; standardization (g - mu)/sigma with the population std
+ * (bed.rs:231-242) is folded into the first-layer weights. */
 
 /* g: variant-major int8 genotypes g[j*n + i] in {0,1,2}; mu/sigma computed on device */
 int bann_genotypes_upload(bann_ctx* ctx, const int8_t* g, int64_t n, int64_t num_markers);
@@ -250,11 +252,50 @@ int bann_leapfrog_residual_delta_device(bann_ctx* ctx, float* out_device);
 /* same, copied to a HOST buffer of n floats (device scratch owned by the context) */
 int bann_leapfrog_residual_delta(bann_ctx* ctx, float* out_host);
 int bann_synchronize(bann_ctx* ctx);
+/* in-trajectory launch timing: while enabled, every gradient and update launch
+ * of a leapfrog session (bann_leapfrog_begin / _steps) is bracketed by HIP
+ * events on the context's stream; bann_leapfrog_end accumulates their elapsed
+ * times.  bann_launch_timing returns the average milliseconds per gradient and
+ * per update launch and the number of gradient launches since the last reset.
+ * (Set outside a session.) */
+int bann_set_launch_timing(bann_ctx* ctx, int32_t enabled);
+int bann_launch_timing(bann_ctx* ctx, float* grad_ms, float* update_ms, int32_t* grad_launches, int32_t reset);
+/* individuals n of the context's cohort */
+int64_t bann_ctx_num_individuals(const bann_ctx* ctx);
 /* measurement hook: times `iters` packed gradient launches and `iters` update
  * launches (gradient-only mode, no state change) of the active leapfrog
  * session's branch set with HIP events on the context's stream; returns the
  * average milliseconds per launch of each. */
 int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms, float* update_ms);
+
+/* ---------------- the network residual on the device ----------------
+ * Net::train keeps the residual y - bias - sum_b f_b as a device Array and
+ * updates it between branch updates (net.rs:158-171, 221, 279-300, 319-332).
+ * The context owns one n-float device residual; every operation below is one
+ * launch on the device (no n-float host copy).  Where a branch's prediction row
+ * is needed and is not current (params set since the last forward pass), the
+ * call first runs one packed forward launch over those branches.  sum / sumsq
+ * (each may be NULL; both NULL = no host synchronisation) receive the sum and
+ * the sum of squares of the residual after the operation, reduced in a fixed
+ * order (deterministic). */
+int bann_residual_set(bann_ctx* ctx, const float* residual);  /* host -> device residual */
+int bann_residual_get(bann_ctx* ctx, float* residual_out);    /* device residual -> host */
+int bann_residual_device(bann_ctx* ctx, float** out);         /* its device pointer (n floats) */
+/* initialize_stats (net.rs:158-171): residual = (y - bias) - f_0 - f_1 - ... (branch order, f32) */
+int bann_residual_init(bann_ctx* ctx, const float* y, float bias, double* sum, double* sumsq);
+int bann_residual_stats(bann_ctx* ctx, double* sum, double* sumsq);
+/* residual += add (the output bias: net.rs:321, 332) */
+int bann_residual_shift(bann_ctx* ctx, float add, double* sum, double* sumsq);
+/* net.rs:279-280: target y_b = residual + f_b(theta_b) */
+int bann_residual_to_target(bann_ctx* ctx, int32_t b);
+/* net.rs:292-300: residual = y_b - f_b(theta_b) after the branch's trajectory
+ * (accepted: f_b(theta_L), i.e. residual -= y_pred; rejected: f_b(theta_0), i.e.
+ * residual -= prev_pred) */
+int bann_residual_from_target(bann_ctx* ctx, int32_t b, double* sum, double* sumsq);
+/* targets of a packed sweep in one launch: y_b = r + f_b(theta_b) for every listed
+ * branch, r = residual_device (n floats on the device) or NULL for the
+ * context's own residual */
+int bann_rebuild_targets(bann_ctx* ctx, const int32_t* branches, int32_t nb, const float* residual_device);
 
 /* ---------------- multi-GPU: branch shards, one process (rank) per GPU ----------------
  * Branches share no weights: a rank owns a contiguous branch
@@ -285,6 +326,9 @@ int bann_residual_update_host(bann_allreduce_fn fn, void* user, float* local_del
 /* after bann_leapfrog_end: residual_host[i] -= (sum over ranks of each rank's
  * bann_leapfrog_residual_delta)[i]; collective over the ranks */
 int bann_exchange_residual(bann_ctx* ctx, float* residual_host);
+/* the same on the context's device residual (bann_residual_*): with RCCL the
+ * change is summed over the ranks on the device, no host copy; collective */
+int bann_exchange_residual_device(bann_ctx* ctx);
 /* network-joint HMC trajectory (SURVEY 8(e) packed-joint mode): the parameters
  * of every branch of every rank form ONE HMC state for
  *   -U = -lambda_e/2 ||sum_b f_b + bias - y||^2 + sum_b log prior_b(theta_b)
@@ -292,24 +336,29 @@ int bann_exchange_residual(bann_ctx* ctx, float* residual_host);
  * of the n-vector sum of their outputs, e = sum f + bias - y as every branch's
  * output error (the summary output and its gradient), a gradient launch and
  * the update.  -H is summed over the ranks; early rejection and the Metropolis
- * test (u) decide for the whole network, identically on every rank.  Collective.
+ * test decide for the whole network, identically on every rank.  Collective.
  *   y: n targets on the host (identical on every rank); step_mode: Izmailov or
  *   uniform (device step sizes from the local precisions) or INJECTED (eps:
  *   the local branches' step sizes, concatenated in branch order); momentum:
  *   concatenated p0 of the local branches or NULL (device N(0,1) from seed; a
- *   rank-distinct stream is the caller's choice of seed); u: the uniform.
- * Outputs (may be NULL): status, h_trace[L+1], rss of the final state. */
+ *   rank-distinct stream is the caller's choice of seed); u: the Metropolis
+ *   uniform (injected, parity runs) or NULL: drawn on rank 0 from seed and
+ *   shared with every rank through the -H all-reduce, so all ranks decide alike.
+ * Per step the first pass over the genotypes is forward-only (the outputs the
+ * all-reduce needs); the gradient pass follows once e is known.
+ * Outputs (may be NULL): status, h_trace[L+1], rss of the final state.  The
+ * branch targets are left as the network targets f_b - e of the last step. */
 int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
                           float max_hamiltonian_error, int32_t step_mode, float step_factor, const float* eps,
-                          const float* momentum, uint64_t seed, float u, int32_t* status_out, double* h_trace_out,
-                          double* rss_out);
+                          const float* momentum, uint64_t seed, const float* u, int32_t* status_out,
+                          double* h_trace_out, double* rss_out);
 
 /* ---------------- introspection for tests / profiling ---------------- */
 /* which gradient kernel serves branch b: 1 = fx fused single-pass kernel (every
  * width <= 4, m <= 512), 3 = fxl (every width <= 4, 512 < m <= 4096: one wave
  * per 512-marker block), 2 = wide fused kernel (one hidden layer, W, S <= 32,
  * m <= 128: masked layer on i8 MFMA, hidden GEMMs on f32 or bf16 MFMA),
- * 0 = generic kernels (any shape) */
+ * 0 = the layered gx path (any depth / widths: batched MFMA GEMMs per layer) */
 int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
 /* name of the fused gradient kernel family used for branches of <= 512 markers */
 const char* bann_fused_kernel_name(void);
@@ -318,7 +367,7 @@ const char* bann_fused_kernel_name(void);
  * "bf16 hidden GEMM on MFMA vs fp32": 16x the matrix rate, bf16 operand
  * rounding (~1e-3 relative on gradients; not parity-exact).  Any time. */
 int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled);
-/* force every branch onto the generic path (0) or allow the fused path (1) */
+/* force every branch onto the layered gx path (0) or allow the fused kernels (1) */
 int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
 /* bytes of packed genotype data read per full gradient evaluation of all branches */
 int64_t bann_packed_genotype_bytes(const bann_ctx* ctx);

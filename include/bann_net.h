@@ -14,12 +14,14 @@
  *   Net::to_file/from_file src/net/net.rs:107-115 (bincode 1.3 legacy encoding of
  *                          the Net<B> struct)
  *
- * The per-branch math (predict, the HMC trajectory, step sizes) runs on the
- * device through bann.h; the Gibbs precision draws, the residual bookkeeping
- * (n floats), the output bias and the log posterior density stay on the host,
- * as in the reference (north_star: "the Gibbs hyperparameter sweep stays on the
- * host").  Same conventions as bann.h: int status codes, host pointers read or
- * written inside the call and never retained.
+ * The per-branch math (predict, the HMC trajectory, step sizes) and the
+ * residual bookkeeping (the context's device residual, bann.h "the network
+ * residual on the device": net.rs keeps it as a device Array too) run on the
+ * device through bann.h; the Gibbs precision draws, the output bias and the log
+ * posterior density -- scalars -- stay on the host, as in the reference
+ * (north_star: "the Gibbs hyperparameter sweep stays on the host").  Same
+ * conventions as bann.h: int status codes, host pointers read or written inside
+ * the call and never retained.
  */
 #ifndef BANN_NET_H
 #define BANN_NET_H
@@ -45,18 +47,22 @@ typedef struct {
 
 /* The MCMCCfg fields (mcmc_cfg.rs:181-204) Net::train reads on its HMC path.
  * Defaults (MCMCCfgBuilder::default, mcmc_cfg.rs:34-56): factor 1, max error 10,
- * L 100, Izmailov, chain 100, burn_in chain-1, precisions sampled, ML bias. */
+ * L 100, Izmailov, chain 100, burn_in chain-1, precisions sampled, ML bias,
+ * no joint HMC. */
 typedef struct {
   float hmc_step_size_factor;
   float hmc_max_hamiltonian_error;
   int32_t hmc_integration_length;
-  int32_t hmc_step_size_mode; /* bann_step_mode: BANN_STEP_IZMAILOV or BANN_STEP_UNIFORM */
+  int32_t hmc_step_size_mode; /* bann_step_mode: BANN_STEP_IZMAILOV, BANN_STEP_UNIFORM or BANN_STEP_RANDOM
+                                 (StepSizeMode, mcmc_cfg.rs:264-270; StdScaled is unusable in the reference) */
   int32_t chain_length;
   int32_t burn_in;
   int32_t fixed_param_precisions;
   int32_t sampled_output_bias;
   int32_t trace;         /* outdir/trace: the BranchCfgs as a JSON line after init and every sweep (net.rs:241-244, 350-353) */
   int32_t trajectories;  /* outdir/traj: one JSON Trajectory line per HMC step (trajectory.rs, branch_sampler.rs:1196-1289) */
+  int32_t joint_hmc;     /* MCMCCfg::joint_hmc: hmc_step_joint over params and precisions, no Gibbs draws
+                            (net.rs:270-290; random step sizes, branch_sampler.rs:1092-1101) */
 } bann_mcmc_cfg;
 
 /* Host random source for the driver's draws (the reference's ThreadRng,
@@ -67,8 +73,12 @@ typedef struct {
  * (one gamma per input node for ARD priors, else one) then the bias precision
  * (1 gamma), then the output-layer precision (1 gamma); the momentum (P
  * normals, param_vec order); the acceptance uniform (1 uniform); then, with
- * sampled output bias, 1 gamma + 1 normal.  Each sweep starts with the branch
- * shuffle: nb-1 uniforms (Fisher-Yates, i = nb-1 .. 1, j = floor(u (i+1))). */
+ * sampled output bias, 1 gamma + 1 normal.  Random step sizes: P uniforms
+ * (param_vec order) before the momentum.  Joint HMC instead: no Gibbs draws;
+ * P + Q uniforms (step sizes, [param_vec | precision_vec]), P + Q normals
+ * (momentum), the acceptance uniform.  Each sweep of bann_net_train starts
+ * with the branch shuffle: nb-1 uniforms (Fisher-Yates, i = nb-1 .. 1,
+ * j = floor(u (i+1))); bann_net_train_single_branch draws no shuffle. */
 typedef struct {
   void* user;
   double (*uniform)(void* user);
@@ -113,11 +123,26 @@ int bann_net_records_test(const bann_net* net, float* mse_test, int32_t cap);
  * models/<chain_ix>.bin after burn-in (net.rs:338-342, 565-569) and
  * training_stats (JSON, train_stats.rs:83-87). */
 int bann_net_train(bann_net* net, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir);
+/* Net::train_single_branch (net.rs:360-507): branch 0 only, one HMC update per
+ * chain iteration, record_perf / model file / trace after every update */
+int bann_net_train_single_branch(bann_net* net, const float* y, int64_t n, const bann_mcmc_cfg* cfg,
+                                 const char* outdir);
+/* Net::perturb (net.rs:187-199, params.rs:219-233, 602-614): add params_by to
+ * every weight and bias and / or precisions_by to every precision of every
+ * branch (has_* = 0: that part untouched), e.g. to restart a loaded chain */
+int bann_net_perturb(bann_net* net, int32_t has_params, float params_by, int32_t has_precisions,
+                     float precisions_by);
+/* Net::predict (net.rs:545-559): y_hat[i] = bias + sum_b f_b (f32, branch order)
+ * on the cohort of ctx, a context with the net's branches (count, markers, layer
+ * widths) -- e.g. a test cohort -- or NULL for the net's own context.  The net's
+ * current parameters are loaded into ctx first. */
+int bann_net_predict(bann_net* net, bann_ctx* ctx, float* y_hat_out);
 int bann_net_summary(const bann_net* net, bann_train_summary* out);
 /* the recorded mse_train / lpd series (TrainingStats::mse_train / lpd);
  * writes min(cap, num_records) entries of each (either may be NULL) */
 int bann_net_records(const bann_net* net, float* mse_train, float* lpd, int32_t cap);
-/* the residual y - bias - sum_b f_b after the last branch update (n floats) */
+/* the residual y - bias - sum_b f_b after the last branch update (n floats,
+ * copied from the context's device residual) */
 int bann_net_residual(const bann_net* net, float* out);
 /* Net::to_file (net.rs:112-115): bincode Net<B> of the current state */
 int bann_net_save(const bann_net* net, const char* path);

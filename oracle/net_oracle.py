@@ -111,8 +111,10 @@ class NetOracle:
             br.bias_precisions[l] = d.gamma(a, s)
 
     def train(self, y, d: Draws, chain_length: int, L_int: int, max_dH: float = 10.0, factor: float = 1.0,
-              step_mode: str = "izmailov", fixed_param_precisions: bool = False, sampled_output_bias: bool = False):
-        """Net::train (net.rs:201-358), HMC path"""
+              step_mode: str = "izmailov", fixed_param_precisions: bool = False, sampled_output_bias: bool = False,
+              joint_hmc: bool = False, single_branch: bool = False):
+        """Net::train (net.rs:201-358), HMC path; single_branch: Net::train_single_branch
+        (net.rs:360-507: branch 0 every chain iteration, a record after every update)."""
         n = y.size
         nb = len(self.br)
         k_out, s_out = self.hp.output
@@ -125,33 +127,50 @@ class NetOracle:
         self._record()
         order = list(range(nb))
         for _chain in range(chain_length):
-            for i in range(nb - 1, 0, -1):   # branch_ixs.shuffle (257)
-                j = min(i, int(math.floor(d.uniform() * (i + 1))))
-                order[i], order[j] = order[j], order[i]
+            if single_branch:
+                order = [0]
+            else:
+                for i in range(nb - 1, 0, -1):   # branch_ixs.shuffle (257)
+                    j = min(i, int(math.floor(d.uniform() * (i + 1))))
+                    order[i], order[j] = order[j], order[i]
             for b in order:
                 br = self.br[b]
                 others = self._from_cfg(b)
-                # sample_error_precision (branch_sampler.rs:190-202)
-                a, s = O.ridge_posterior_params(k_out, s_out, float(np.sum(self.residual ** 2)), n)
-                br.error_precision = d.gamma(a, s)
-                if not fixed_param_precisions:   # sample_param_precisions (173-188)
-                    self._sample_prior_precisions(br, d)
-                    total = others + out_stat(br)
-                    post = O.lasso_posterior_params if br.prior.startswith("lasso") else O.ridge_posterior_params
-                    a, s = post(k_out, s_out, total, self.g_num)
-                    br.weight_precisions[-1] = np.array([d.gamma(a, s)])
+                if not joint_hmc:   # 270-277
+                    # sample_error_precision (branch_sampler.rs:190-202)
+                    a, s = O.ridge_posterior_params(k_out, s_out, float(np.sum(self.residual ** 2)), n)
+                    br.error_precision = d.gamma(a, s)
+                    if not fixed_param_precisions:   # sample_param_precisions (173-188)
+                        self._sample_prior_precisions(br, d)
+                        total = others + out_stat(br)
+                        post = O.lasso_posterior_params if br.prior.startswith("lasso") else O.ridge_posterior_params
+                        a, s = post(k_out, s_out, total, self.g_num)
+                        br.weight_precisions[-1] = np.array([d.gamma(a, s)])
                 prev = O.predict(br, self.X[b])                                   # 279-280
                 self.residual = self.residual + prev
                 target = self.residual.astype(np.float32).astype(np.float64)      # the f32 target on the device
-                p = np.array([d.normal() for _ in range(br.num_params)])
-                u = d.uniform()
-                p_w, p_b = O.load_param_vec(p.astype(np.float32).astype(np.float64), br.num_markers,
-                                            br.layer_widths)
-                if step_mode == "izmailov":
-                    ew, eb = O.izmailov_step_sizes(br, factor, L_int)
+                f32 = lambda v: np.float64(np.float32(v))   # noqa: E731  (the device's f32 draws)
+                if joint_hmc:   # hmc_step_joint (branch_sampler.rs:1070-1178), random step sizes (654-704)
+                    P, Q = br.num_params, O.precision_vec(br).size
+                    f = np.float32(np.float32(P + Q) ** np.float32(-0.25)) * np.float32(factor)
+                    eps = np.array([f32(np.float32(d.uniform()) * f) for _ in range(P + Q)])
+                    p = np.array([f32(d.normal()) for _ in range(P + Q)])
+                    u = f32(d.uniform())
+                    out = O.hmc_step_joint(br, self.X[b], target, self.hp, eps, p, L_int, max_dH, u)
                 else:
-                    ew, eb = O.uniform_step_sizes(br, factor)
-                out = O.hmc_step(br, self.X[b], target, ew, eb, p_w, p_b, L_int, max_dH, u)
+                    if step_mode == "random":   # random_step_sizes (654-681): drawn before the momentum
+                        f = np.float32(np.float32(br.num_params) ** np.float32(-0.25)) * np.float32(factor)
+                        ev = np.array([f32(np.float32(d.uniform()) * f) for _ in range(br.num_params)])
+                        ew, eb = O.load_param_vec(ev, br.num_markers, br.layer_widths)
+                    p = np.array([d.normal() for _ in range(br.num_params)])
+                    u = f32(d.uniform())
+                    p_w, p_b = O.load_param_vec(p.astype(np.float32).astype(np.float64), br.num_markers,
+                                                br.layer_widths)
+                    if step_mode == "izmailov":
+                        ew, eb = O.izmailov_step_sizes(br, factor, L_int)
+                    elif step_mode == "uniform":
+                        ew, eb = O.uniform_step_sizes(br, factor)
+                    out = O.hmc_step(br, self.X[b], target, ew, eb, p_w, p_b, L_int, max_dH, u)
                 self.ns += 1
                 self.nacc += out["status"] == O.ACCEPTED
                 self.nearly += out["status"] == O.REJECTED_EARLY
@@ -176,7 +195,10 @@ class NetOracle:
                 else:
                     self.ob_bias = sr / n
                 self.residual = self.residual - self.ob_bias
-            self._record()
+                if single_branch:
+                    self._record()
+            if not single_branch:
+                self._record()
 
 
 # ------------------------------------------------------------------ model file

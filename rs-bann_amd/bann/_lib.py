@@ -52,7 +52,8 @@ class McmcCfg(C.Structure):
     _fields_ = [("hmc_step_size_factor", C.c_float), ("hmc_max_hamiltonian_error", C.c_float),
                 ("hmc_integration_length", C.c_int32), ("hmc_step_size_mode", C.c_int32),
                 ("chain_length", C.c_int32), ("burn_in", C.c_int32), ("fixed_param_precisions", C.c_int32),
-                ("sampled_output_bias", C.c_int32), ("trace", C.c_int32), ("trajectories", C.c_int32)]
+                ("sampled_output_bias", C.c_int32), ("trace", C.c_int32), ("trajectories", C.c_int32),
+                ("joint_hmc", C.c_int32)]
 
 
 # bann_allreduce_fn: in-place sum over ranks of a host buffer (dtype 0 f32, 1 f64)
@@ -121,8 +122,21 @@ SIGNATURES = {
     "bann_ctx_comm_callback": (C.c_int, [_P, ALLREDUCE_FN, _P, _i32, _i32]),
     "bann_residual_update_host": (C.c_int, [ALLREDUCE_FN, _P, _pf32, _pf32, _i64]),
     "bann_exchange_residual": (C.c_int, [_P, _pf32]),
-    "bann_network_hmc_step": (C.c_int, [_P, _pf32, _f32, _f32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _f32,
+    "bann_network_hmc_step": (C.c_int, [_P, _pf32, _f32, _f32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32,
                                         _pi32, _pf64, _pf64]),
+    "bann_exchange_residual_device": (C.c_int, [_P]),
+    "bann_residual_set": (C.c_int, [_P, _pf32]),
+    "bann_residual_get": (C.c_int, [_P, _pf32]),
+    "bann_residual_device": (C.c_int, [_P, C.POINTER(_pf32)]),
+    "bann_residual_init": (C.c_int, [_P, _pf32, _f32, _pf64, _pf64]),
+    "bann_residual_stats": (C.c_int, [_P, _pf64, _pf64]),
+    "bann_residual_shift": (C.c_int, [_P, _f32, _pf64, _pf64]),
+    "bann_residual_to_target": (C.c_int, [_P, _i32]),
+    "bann_residual_from_target": (C.c_int, [_P, _i32, _pf64, _pf64]),
+    "bann_rebuild_targets": (C.c_int, [_P, _pi32, _i32, _P]),
+    "bann_set_launch_timing": (C.c_int, [_P, _i32]),
+    "bann_launch_timing": (C.c_int, [_P, _pf32, _pf32, _pi32, _i32]),
+    "bann_ctx_num_individuals": (_i64, [_P]),
     "bann_leapfrog_begin": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _u64]),
     "bann_leapfrog_steps": (C.c_int, [_P, _i32]),
     "bann_leapfrog_end": (C.c_int, [_P, _pi32, _pi32]),
@@ -144,6 +158,9 @@ SIGNATURES = {
     "bann_net_set_rng_hooks": (C.c_int, [_P, C.POINTER(RngHooks)]),
     "bann_net_set_global": (C.c_int, [_P, _f32, _f32, _f32, _f32]),
     "bann_net_train": (C.c_int, [_P, _pf32, _i64, C.POINTER(McmcCfg), C.c_char_p]),
+    "bann_net_train_single_branch": (C.c_int, [_P, _pf32, _i64, C.POINTER(McmcCfg), C.c_char_p]),
+    "bann_net_perturb": (C.c_int, [_P, _i32, _f32, _i32, _f32]),
+    "bann_net_predict": (C.c_int, [_P, _P, _pf32]),
     "bann_net_summary": (C.c_int, [_P, C.POINTER(TrainSummary)]),
     "bann_net_records": (C.c_int, [_P, _pf32, _pf32, _i32]),
     "bann_net_residual": (C.c_int, [_P, _pf32]),

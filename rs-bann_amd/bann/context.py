@@ -320,9 +320,12 @@ class BannContext:
 
     def network_hmc_step(self, y, L: int, bias: float = 0.0, lambda_e: float = 1.0,
                          max_hamiltonian_error: float = 10.0, step_mode: str = "izmailov",
-                         step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0, u: float = 0.5):
+                         step_factor: float = 1.0, eps=None, momentum=None, seed: int = 0,
+                         u: Optional[float] = None):
         """network-joint HMC trajectory over every branch of every rank (collective).
-        eps / momentum: concatenated over this context's branches in branch order (or None)."""
+        eps / momentum: concatenated over this context's branches in branch order (or None);
+        u: injected Metropolis uniform (parity runs) or None: drawn on rank 0 from seed and
+        shared with every rank by the library."""
         ya = _f32(y)
         if ya.size != self.n:
             raise ValueError(f"y has {ya.size} entries, n = {self.n}")
@@ -338,9 +341,65 @@ class BannContext:
         self._check(self._lib.bann_network_hmc_step(
             self._h, _ptr(ya, C.c_float), bias, lambda_e, L, max_hamiltonian_error, mode, step_factor,
             _ptr(eps_a, C.c_float) if eps_a is not None else nullf,
-            _ptr(mom_a, C.c_float) if mom_a is not None else nullf, seed, u, C.byref(st), _ptr(tr, C.c_double),
+            _ptr(mom_a, C.c_float) if mom_a is not None else nullf, seed,
+            C.byref(C.c_float(u)) if u is not None else nullf, C.byref(st), _ptr(tr, C.c_double),
             C.byref(rss)))
         return dict(status=st.value, trace=tr, rss=rss.value)
+
+    def exchange_residual_device(self):
+        """device residual -= sum over ranks of the last session's residual change (collective)."""
+        self._check(self._lib.bann_exchange_residual_device(self._h))
+
+    # ------------------------------------------------ device residual (net.rs:158-332)
+    def residual_set(self, r):
+        v = _f32(r)
+        assert v.size == self.n
+        self._check(self._lib.bann_residual_set(self._h, _ptr(v, C.c_float)))
+
+    def residual_get(self) -> np.ndarray:
+        out = np.zeros(self.n, np.float32)
+        self._check(self._lib.bann_residual_get(self._h, _ptr(out, C.c_float)))
+        return out
+
+    def residual_init(self, y, bias: float = 0.0):
+        """residual = (y - bias) - sum_b f_b (initialize_stats); returns (sum, sum of squares)."""
+        v = _f32(y)
+        s, q = C.c_double(), C.c_double()
+        self._check(self._lib.bann_residual_init(self._h, _ptr(v, C.c_float), float(bias), C.byref(s), C.byref(q)))
+        return s.value, q.value
+
+    def residual_stats(self):
+        s, q = C.c_double(), C.c_double()
+        self._check(self._lib.bann_residual_stats(self._h, C.byref(s), C.byref(q)))
+        return s.value, q.value
+
+    def residual_shift(self, add: float):
+        s, q = C.c_double(), C.c_double()
+        self._check(self._lib.bann_residual_shift(self._h, float(add), C.byref(s), C.byref(q)))
+        return s.value, q.value
+
+    def residual_to_target(self, b: int):
+        self._check(self._lib.bann_residual_to_target(self._h, b))
+
+    def residual_from_target(self, b: int):
+        s, q = C.c_double(), C.c_double()
+        self._check(self._lib.bann_residual_from_target(self._h, b, C.byref(s), C.byref(q)))
+        return s.value, q.value
+
+    def rebuild_targets(self, branches, residual_device_ptr: int = 0):
+        """y_b = r + f_b for every listed branch in one launch (r: the context's residual, or a device pointer)."""
+        bl = np.ascontiguousarray(branches, dtype=np.int32)
+        self._check(self._lib.bann_rebuild_targets(self._h, _ptr(bl, C.c_int32), bl.size,
+                                                   C.c_void_p(residual_device_ptr or None)))
+
+    def set_launch_timing(self, enabled: bool):
+        self._check(self._lib.bann_set_launch_timing(self._h, 1 if enabled else 0))
+
+    def launch_timing(self, reset: bool = True):
+        """(grad_ms, update_ms, grad_launches): averages over the timed leapfrog-session launches."""
+        g, u, k = C.c_float(), C.c_float(), C.c_int32()
+        self._check(self._lib.bann_launch_timing(self._h, C.byref(g), C.byref(u), C.byref(k), 1 if reset else 0))
+        return g.value, u.value, k.value
 
     # ------------------------------------------------------ leapfrog session
     def leapfrog_begin(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,

@@ -36,13 +36,14 @@ class MCMCConfig:
     sampled_output_bias: bool = False
     trace: bool = False          # outdir/trace: BranchCfgs as JSON per sweep (net.rs:241-244, 350-353)
     trajectories: bool = False   # outdir/traj: one Trajectory JSON per HMC step (trajectory.rs)
+    joint_hmc: bool = False      # hmc_step_joint over params and precisions, no Gibbs draws (net.rs:270-290)
 
     def to_c(self) -> McmcCfg:
         burn = self.chain_length - 1 if self.burn_in is None else self.burn_in
         return McmcCfg(self.hmc_step_size_factor, self.hmc_max_hamiltonian_error, self.hmc_integration_length,
                        STEP_MODES[self.hmc_step_size_mode], self.chain_length, max(burn, 0),
                        int(self.fixed_param_precisions), int(self.sampled_output_bias), int(self.trace),
-                       int(self.trajectories))
+                       int(self.trajectories), int(self.joint_hmc))
 
 
 class Net:
@@ -95,6 +96,25 @@ class Net:
         v = np.ascontiguousarray(y, dtype=np.float32)
         self._check(self._lib.bann_net_train(self._h, v.ctypes.data_as(C.POINTER(C.c_float)), v.size,
                                              C.byref(cfg.to_c()), outdir.encode() if outdir else None))
+
+    def train_single_branch(self, y, cfg: MCMCConfig = MCMCConfig(), outdir: Optional[str] = None):
+        """Net::train_single_branch (net.rs:360-507): branch 0, one update per chain iteration."""
+        v = np.ascontiguousarray(y, dtype=np.float32)
+        self._check(self._lib.bann_net_train_single_branch(self._h, v.ctypes.data_as(C.POINTER(C.c_float)), v.size,
+                                                           C.byref(cfg.to_c()), outdir.encode() if outdir else None))
+
+    def perturb(self, params_by: Optional[float] = None, precisions_by: Optional[float] = None):
+        """Net::perturb (net.rs:187-199): shift every param and / or precision by a constant."""
+        self._check(self._lib.bann_net_perturb(self._h, int(params_by is not None), float(params_by or 0.0),
+                                               int(precisions_by is not None), float(precisions_by or 0.0)))
+
+    def predict(self, ctx=None) -> np.ndarray:
+        """Net::predict (net.rs:545-559): bias + sum_b f_b on ctx's cohort (default: the training context)."""
+        c = ctx if ctx is not None else self._ctx
+        out = np.zeros(c.n, np.float32)
+        self._check(self._lib.bann_net_predict(self._h, c._h if ctx is not None else None,
+                                               out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
 
     def summary(self) -> dict:
         s = TrainSummary()

@@ -329,36 +329,78 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
   return BANN_OK;
 }
 
-// gradient (partials) of every branch in the plan at the current theta
+// gradient (partials) of every branch in the plan at the current theta.
+// write_pred: 0 = no predictions (the layered path writes them anyway), 1 = the
+// predictions f_b(theta) into pred, 2 = into pred0 (a trajectory's start: the
+// restore copy and the residual change read them there)
 int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
+  DevState s = ctx->st;
+  if (write_pred == 2) s.pred = ctx->d_pred0;
+  const int wp = write_pred != 0;
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
-      launch_fused_grad_wx(ctx->st, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, write_pred, ctx->stream);
+      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, wp, ctx->stream);
     else if (g.kind == 3)
-      launch_fused_grad_fxl(ctx->st, g.d_items, ni, g.L, g.act, g.nw, g.full, write_pred, ctx->stream);
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, wp, ctx->stream);
     else
-      launch_fused_grad_fx(ctx->st, g.d_items, ni, g.L, g.act, g.full, write_pred, ctx->stream);
+      launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, ctx->stream);
   }
-  if (!p.fold.empty()) launch_fold_solo(ctx->st, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
+  if (!p.fold.empty()) launch_fold_solo(s, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
   // gx branches: scratch group by scratch group (the groups reuse one scratch)
   for (const auto& g : p.gxg) {
     const int32_t* bl = p.d_gx + g.first;
-    launch_gx_prep(ctx->st, bl, g.count, ctx->stream);
+    launch_gx_prep(s, bl, g.count, ctx->stream);
     for (const auto& ph : g.phases) {
       if (ph.ph == GX_HEAD)
-        launch_gx_head(ctx->st, bl, g.count, g.max_splits, ctx->stream);
+        launch_gx_head(s, bl, g.count, g.max_splits, ctx->stream);
       else
-        launch_gx_gemm(ctx->st, ph.ph, ph.l, bl, p.d_gxpre + ph.pre_off, g.count, ph.total, ctx->stream);
+        launch_gx_gemm(s, ph.ph, ph.l, bl, p.d_gxpre + ph.pre_off, g.count, ph.total, ctx->stream);
     }
   }
   CK(hipGetLastError());
+  if (write_pred == 1) mark_predictions(ctx, p, true);
   return BANN_OK;
+}
+
+// predictions f_b(theta) of every branch in the plan: fx groups through the
+// forward-only kernel (no target, no backward), every other path through its
+// gradient launch with predictions (their partial slabs are scratch here)
+int run_forward(bann_ctx* ctx, const Plan& p) {
+  const DevState& s = ctx->st;
+  for (const auto& g : p.groups) {
+    const int32_t ni = (int32_t)g.items.size();
+    if (g.kind == 2)
+      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, 1, ctx->stream);
+    else if (g.kind == 3)
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, 1, ctx->stream);
+    else
+      launch_forward_fx(s, g.d_items, ni, g.L, g.act, g.full, ctx->stream);
+  }
+  for (const auto& g : p.gxg) {
+    const int32_t* bl = p.d_gx + g.first;
+    launch_gx_prep(s, bl, g.count, ctx->stream);
+    for (const auto& ph : g.phases) {
+      if (ph.ph == GX_HEAD) {
+        launch_gx_head(s, bl, g.count, g.max_splits, ctx->stream);
+        break;  // the head writes the predictions; the backward phases are not needed
+      }
+      launch_gx_gemm(s, ph.ph, ph.l, bl, p.d_gxpre + ph.pre_off, g.count, ph.total, ctx->stream);
+    }
+  }
+  CK(hipGetLastError());
+  mark_predictions(ctx, p, true);
+  return BANN_OK;
+}
+
+void mark_predictions(bann_ctx* ctx, const Plan& p, bool current) {
+  for (int32_t b : p.all) ctx->pred_ok[b] = current;
 }
 
 // the fused leapfrog update of every branch in the plan (small and large kernels)
 void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step) {
   const int32_t nb = (int32_t)p.all.size();
+  if (mode != MODE_GRAD && mode != MODE_PROFILE) mark_predictions(ctx, p, false);  // theta moves
   launch_update(ctx->st, p.d_all + nb, p.n_small, mode, step, ctx->stream, 0);
   launch_update(ctx->st, p.d_all + nb + p.n_small, p.n_large, mode, step, ctx->stream, 1);
 }
@@ -414,11 +456,14 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
                   ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_fold_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
-                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart};
+                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res,
+                  ctx->d_res_part};
+  for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
   comm_destroy(ctx);
   for (void* p : bufs) dfree(p);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
+  if (ctx->h_res_stat) (void)hipHostFree(ctx->h_res_stat);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BANN_OK;
@@ -632,6 +677,7 @@ extern "C" const char* bann_fused_kernel_name(void) { return "k_fused_grad_fx"; 
 extern "C" int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled) {
   if (!ctx) return BANN_E_ARG;
   ctx->wide_bf16 = enabled != 0;
+  std::fill(ctx->pred_ok.begin(), ctx->pred_ok.end(), 0);  // wide-branch predictions change with the GEMM precision
   return BANN_OK;
 }
 extern "C" int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled) {
@@ -935,6 +981,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     CK(hipMemsetAsync(ctx->d_dbg, 0, 16 * sizeof(unsigned long long), ctx->stream));
   }
   ctx->finalized = true;
+  ctx->pred_ok.assign(ctx->br.size(), 0);
   int rc = ensure_htrace(ctx, 1);
   if (rc) return rc;
   refresh_state(ctx);
@@ -957,6 +1004,7 @@ extern "C" int bann_branch_set_params(bann_ctx* ctx, int32_t b, const float* par
   launch_fused_const(ctx->st, ctx->d_list_scr, 1, ctx->stream);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
+  ctx->pred_ok[b] = 0;
   return BANN_OK;
 }
 
@@ -1049,7 +1097,8 @@ static int eval_branch(bann_ctx* ctx, int32_t b, int write_pred) {
 
 extern "C" int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out) {
   if (!check_branch(ctx, b) || !pred_out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
-  int rc = eval_branch(ctx, b, 1);
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  int rc = ensure_predictions(ctx, &b, 1);
   if (rc) return rc;
   CK(hipMemcpyAsync(pred_out, ctx->d_pred + (int64_t)b * ctx->n, ctx->n * sizeof(float), hipMemcpyDeviceToHost,
                     ctx->stream));
@@ -1060,10 +1109,11 @@ extern "C" int bann_predict(bann_ctx* ctx, int32_t b, float* pred_out) {
 extern "C" int bann_predict_many(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* pred_out) {
   if (!ctx || !branches || nb <= 0 || !pred_out) return fail(ctx, BANN_E_ARG, "bad branch list or null output");
   if (!ctx->finalized) return fail(ctx, BANN_E_STATE, "call bann_finalize first");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
   Plan p;
   int rc = build_plan(ctx, branches, nb, p, false);
   if (rc) return rc;
-  rc = run_grad(ctx, p, 1);  // one packed launch per kernel group, predictions written on the way
+  rc = run_forward(ctx, p);  // one packed forward launch per kernel group
   if (rc) return rc;
   for (int32_t i = 0; i < nb; ++i)
     CK(hipMemcpyAsync(pred_out + (int64_t)i * ctx->n, ctx->d_pred + (int64_t)branches[i] * ctx->n,
@@ -1203,7 +1253,7 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   if (rc) return rc;
   rc = traj_prepare(ctx, p, std::max(L, 1), max_dh, step_mode, factor, eps, momentum, seed, u);
   if (rc) return rc;
-  rc = run_grad(ctx, p, L == 0 ? 1 : 0);
+  rc = run_grad(ctx, p, L == 0 ? 1 : 2);  // f(theta_0) -> pred0 (restore copy of a rejected branch)
   if (rc) return rc;
   if (L == 0) {  // empty leapfrog loop: accept_or_reject at the initial state accepts
     run_update(ctx, p, MODE_GRAD, 0);
@@ -1244,6 +1294,9 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
                           h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
       }
   }
+  // rejected branches are back at theta_0: their prediction rows go back to f(theta_0)
+  launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);
+  mark_predictions(ctx, p, true);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
   const int stride = ctx->htrace_cap;
@@ -1334,14 +1387,16 @@ extern "C" int bann_hmc_step_joint(bann_ctx* ctx, const int32_t* branches, int32
     launch_sample_momentum_joint(ctx->st, p.d_all, nb, max_q, seed, ctx->stream);
   }
   CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
-  rc = run_grad(ctx, p, 0);
+  rc = run_grad(ctx, p, 2);  // f(theta_0) -> pred0
   if (rc) return rc;
   launch_update_joint(ctx->st, p.d_all, nb, MODE_INIT, 0, ctx->stream);
   for (int k = 1; k <= L; ++k) {
-    rc = run_grad(ctx, p, 0);
+    rc = run_grad(ctx, p, k == L ? 1 : 0);
     if (rc) return rc;
     launch_update_joint(ctx->st, p.d_all, nb, k < L ? MODE_STEP : MODE_LAST, k, ctx->stream);
   }
+  launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);  // rejected: predictions back to f(theta_0)
+  mark_predictions(ctx, p, true);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
   const int stride = ctx->htrace_cap;
@@ -1381,6 +1436,63 @@ extern "C" int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap,
   return BANN_OK;
 }
 
+// ---- in-trajectory launch timing (bann_set_launch_timing) ----
+// an event after every launch boundary of the session: kind 0 before a gradient
+// launch, 1 between the gradient and the update launch, 2 after the update
+static void tm_mark(bann_ctx* ctx, int32_t kind) {
+  if (!ctx->tm_on) return;
+  const size_t k = ctx->tm_marks.size();
+  if (k == ctx->tm_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;  // timing is best effort: no event, no sample
+    ctx->tm_pool.push_back(e);
+  }
+  if (hipEventRecord(ctx->tm_pool[k], ctx->stream) != hipSuccess) return;
+  ctx->tm_marks.push_back({(int32_t)k, kind});
+}
+
+// after the stream has drained: elapsed times of the gradient (0 -> 1) and update (1 -> 2) launches
+static int tm_resolve(bann_ctx* ctx) {
+  for (size_t i = 0; i + 1 < ctx->tm_marks.size(); ++i) {
+    const auto a = ctx->tm_marks[i], b = ctx->tm_marks[i + 1];
+    if (!((a.second == 0 && b.second == 1) || (a.second == 1 && b.second == 2))) continue;
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, ctx->tm_pool[a.first], ctx->tm_pool[b.first]));
+    if (a.second == 0) {
+      ctx->tm_grad_ms += ms;
+      ++ctx->tm_grad_n;
+    } else {
+      ctx->tm_upd_ms += ms;
+      ++ctx->tm_upd_n;
+    }
+  }
+  ctx->tm_marks.clear();
+  return BANN_OK;
+}
+
+extern "C" int bann_set_launch_timing(bann_ctx* ctx, int32_t enabled) {
+  if (!ctx) return BANN_E_ARG;
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  ctx->tm_on = enabled != 0;
+  ctx->tm_marks.clear();
+  return BANN_OK;
+}
+
+extern "C" int bann_launch_timing(bann_ctx* ctx, float* grad_ms, float* update_ms, int32_t* grad_launches,
+                                  int32_t reset) {
+  if (!ctx) return BANN_E_ARG;
+  if (grad_ms) *grad_ms = ctx->tm_grad_n ? (float)(ctx->tm_grad_ms / ctx->tm_grad_n) : 0.f;
+  if (update_ms) *update_ms = ctx->tm_upd_n ? (float)(ctx->tm_upd_ms / ctx->tm_upd_n) : 0.f;
+  if (grad_launches) *grad_launches = ctx->tm_grad_n;
+  if (reset) {
+    ctx->tm_grad_ms = ctx->tm_upd_ms = 0.0;
+    ctx->tm_grad_n = ctx->tm_upd_n = 0;
+  }
+  return BANN_OK;
+}
+
+extern "C" int64_t bann_ctx_num_individuals(const bann_ctx* ctx) { return ctx ? ctx->n : BANN_E_ARG; }
+
 extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
                                    int32_t step_mode, float factor, uint64_t seed) {
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
@@ -1395,10 +1507,12 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
   }
   rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
   if (rc) return rc;
-  rc = run_grad(ctx, ctx->lf, 1);
+  tm_mark(ctx, 0);
+  rc = run_grad(ctx, ctx->lf, 2);  // f(theta_0) straight into pred0 (the restore copy and the residual change)
   if (rc) return rc;
-  launch_snapshot_pred(ctx->st, ctx->lf.d_all, nb, ctx->stream);
+  tm_mark(ctx, 1);
   run_update(ctx, ctx->lf, MODE_INIT, 0);
+  tm_mark(ctx, 2);
   CK(hipGetLastError());
   ctx->lf_active = true;
   ctx->lf_L = L;
@@ -1412,9 +1526,12 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   const int32_t nb = (int32_t)ctx->lf.all.size();
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
+    tm_mark(ctx, 0);
     int rc = run_grad(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0);
     if (rc) return rc;
+    tm_mark(ctx, 1);
     run_update(ctx, ctx->lf, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
+    tm_mark(ctx, 2);
   }
   CK(hipGetLastError());
   return BANN_OK;
@@ -1428,9 +1545,14 @@ extern "C" int bann_leapfrog_end(bann_ctx* ctx, int32_t* status_out, int32_t* nu
   }
   // rejected branches were restored to theta_0: their prediction rows go back to f(theta_0)
   launch_restore_pred(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->stream);
+  mark_predictions(ctx, ctx->lf, true);
   CK(hipMemcpyAsync(ctx->h_status, ctx->d_status, ctx->br.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
                     ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
+  {
+    int rc = tm_resolve(ctx);
+    if (rc) return rc;
+  }
   const int32_t* st = ctx->h_status;
   int acc = 0;
   for (size_t i = 0; i < ctx->lf.all.size(); ++i) {

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <random>
 #include <vector>
 
 #include <rccl/rccl.h>
@@ -109,20 +110,23 @@ static int allreduce_device_f32(bann_ctx* ctx, float* d, int64_t n) {
   return BANN_OK;
 }
 
-// in-place sum over the ranks of n doubles in a HOST buffer
+// in-place sum over the ranks of n doubles in a HOST buffer (RCCL: through a
+// context-owned device buffer, grown geometrically, not allocated per call)
 static int allreduce_host_f64(bann_ctx* ctx, double* h, int64_t n) {
   if (ctx->comm_kind == 1) {
-    double* d = nullptr;
-    CK(dalloc(&d, n));
+    if (ctx->ar64_cap < n) {
+      dfree(ctx->d_ar64);
+      ctx->d_ar64 = nullptr;
+      const int64_t cap = std::max<int64_t>(n, 2 * ctx->ar64_cap);
+      CK(dalloc(&ctx->d_ar64, cap));
+      ctx->ar64_cap = cap;
+    }
+    double* d = ctx->d_ar64;
     CK(hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     const ncclResult_t r = ncclAllReduce(d, d, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)ctx->nccl, ctx->stream);
-    if (r != ncclSuccess) {
-      dfree(d);
-      return fail(ctx, BANN_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    }
+    if (r != ncclSuccess) return fail(ctx, BANN_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     CK(hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     CK(hipStreamSynchronize(ctx->stream));
-    dfree(d);
   } else if (ctx->comm_kind == 2) {
     if (ctx->ar_fn(ctx->ar_user, h, n, 1) != 0) return fail(ctx, BANN_E_HIP, "all-reduce callback failed");
   }
@@ -146,9 +150,27 @@ extern "C" int bann_exchange_residual(bann_ctx* ctx, float* residual_host) {
   return rc ? fail(ctx, rc, "residual exchange failed") : BANN_OK;
 }
 
+// d_res -= sum over ranks of the last session's residual change, on the device
+// (net.rs:292-300 over ranks; with RCCL no host copy at all)
+extern "C" int bann_exchange_residual_device(bann_ctx* ctx) {
+  if (!ctx) return BANN_E_ARG;
+  if (ctx->lf.all.empty() || ctx->lf_active) return fail(ctx, BANN_E_STATE, "call after bann_leapfrog_end");
+  float* res = nullptr;
+  int rc = bann_residual_device(ctx, &res);
+  if (rc) return rc;
+  launch_residual_delta(ctx->st, ctx->lf.d_all, (int32_t)ctx->lf.all.size(), ctx->d_delta_part, ctx->d_delta,
+                        ctx->stream);
+  CK(hipGetLastError());
+  rc = allreduce_device_f32(ctx, ctx->d_delta, ctx->n);
+  if (rc) return rc;
+  launch_residual_sub(res, ctx->d_delta, ctx->n, ctx->stream);
+  CK(hipGetLastError());
+  return BANN_OK;
+}
+
 extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
                                      float max_dh, int32_t step_mode, float factor, const float* eps,
-                                     const float* momentum, uint64_t seed, float u, int32_t* status_out,
+                                     const float* momentum, uint64_t seed, const float* u, int32_t* status_out,
                                      double* h_trace_out, double* rss_out) {
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
   if (!y || L < 1) return fail(ctx, BANN_E_ARG, "null targets or L < 1");
@@ -183,7 +205,7 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   ctx->st.net_le = lambda_e;
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
   auto forward_and_targets = [&](int k) -> int {
-    int r = run_grad(ctx, p, 1);
+    int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
     if (r) return r;
     launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->stream);
     r = allreduce_device_f32(ctx, ctx->d_netsum, n);
@@ -204,15 +226,26 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   ctx->st.netmode = 0;
   if (rc) return rc;
   CK(hipGetLastError());
-  // network -H per step: sum over local branches (list order) and ranks, plus the rss term once
-  std::vector<double> tr((size_t)nb * ctx->htrace_cap), rss(L + 1), H(L + 1, 0.0);
+  // network -H per step: sum over local branches (list order) and ranks, plus the rss term once.
+  // The Metropolis uniform rides along as entry L + 1: rank 0's draw (or the
+  // injected u), zero elsewhere, so every rank decides with the same u.
+  std::vector<double> tr((size_t)nb * ctx->htrace_cap), rss(L + 1), H(L + 2, 0.0);
   CK(hipMemcpyAsync(tr.data(), ctx->d_htrace, tr.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipMemcpyAsync(rss.data(), ctx->d_netrss, (L + 1) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   for (int k = 0; k <= L; ++k)
     for (int b = 0; b < nb; ++b) H[k] += tr[(size_t)b * ctx->htrace_cap + k];
-  rc = allreduce_host_f64(ctx, H.data(), L + 1);
+  if (ctx->rank == 0) {
+    if (u) {
+      H[L + 1] = (double)*u;
+    } else {  // accept_or_reject_hmc_state's ThreadRng draw (branch_sampler.rs:546-548), from the seed
+      std::mt19937_64 g(seed ^ 0x9E3779B97F4A7C15ull);
+      H[L + 1] = std::uniform_real_distribution<double>(0.0, 1.0)(g);
+    }
+  }
+  rc = allreduce_host_f64(ctx, H.data(), L + 2);
   if (rc) return rc;
+  const double u_net = H[L + 1];
   for (int k = 0; k <= L; ++k) H[k] -= (double)lambda_e * rss[k] / 2.0;  // log_density_wrt_rss (100-102), once
   int status = BANN_ACCEPTED;
   for (int k = 1; k <= L; ++k)
@@ -223,7 +256,7 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   if (status == BANN_ACCEPTED) {  // one Metropolis decision for the network (928-962)
     const double log_acc = H[L] - H[0];
     const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
-    status = (double)u < acc_p ? BANN_ACCEPTED : BANN_REJECTED;
+    status = u_net < acc_p ? BANN_ACCEPTED : BANN_REJECTED;
   }
   std::vector<int32_t> st(nb, status);
   CK(hipMemcpyAsync(ctx->d_status, st.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
@@ -231,10 +264,11 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
     run_update(ctx, p, MODE_RESTORE, 0);
     launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);
   }
+  mark_predictions(ctx, p, true);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
   if (status_out) *status_out = status;
-  if (h_trace_out) std::copy(H.begin(), H.end(), h_trace_out);
+  if (h_trace_out) std::copy(H.begin(), H.begin() + L + 1, h_trace_out);  // H[L + 1] is the shared uniform
   if (rss_out) *rss_out = rss[L];
   return BANN_OK;
 }

@@ -185,6 +185,9 @@ void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nit
                           int write_pred, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, hipStream_t s);
+// forward-only fx pass (predictions into st.pred, no target / backward / partials)
+void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act, int full8,
+                       hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                            int32_t nw, int full, int write_pred, hipStream_t s);
 int fxl_lds_bytes(int nw, int nl);

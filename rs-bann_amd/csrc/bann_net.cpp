@@ -4,10 +4,10 @@
 // bincode Net<B> model file.
 //
 // Host C++ only.  Every per-branch computation (predict, the HMC trajectory with
-// its device step sizes and gradients) goes through the bann.h entry points;
-// what stays here is what the reference also runs on the host between branch
-// updates: n-float residual bookkeeping, Gamma/Normal draws from host RNG,
-// scalar log-density terms (net.rs:201-358).
+// its device step sizes and gradients) and the residual bookkeeping (the
+// context's device residual) go through the bann.h entry points; what stays
+// here is what the reference also keeps on the host between branch updates:
+// Gamma/Normal draws from host RNG and scalar log-density terms (net.rs:201-358).
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -20,6 +20,8 @@
 #include <vector>
 
 #include "../../include/bann_net.h"
+
+#define BANN_NET_MAXL 64  // layer widths read back per branch (bann_branch_info)
 
 namespace {
 
@@ -132,7 +134,7 @@ struct bann_net {
   std::string err;
   std::vector<Branch> br;
   int64_t n = 0;
-  std::vector<float> residual;
+  double rss_cur = 0.0;  // sum of squares of the context's device residual after the last operation
   // GlobalParams (params.rs:13-18)
   float g_eprec = 2.f, g_oprec = 0.05f, g_reg_sum = 0.f;
   uint64_t g_num = 0;
@@ -299,12 +301,13 @@ double ld_joint_out(const bann_net* t, const Branch& B, double others) {
   return -(0.5 * (B.out_stat() + others) + 1.0 / scale) * lam + (shape + (num - 2.0) / 2.0) * std::log(lam);
 }
 
-// LogPosteriorDensity::update_from_branch (log_posterior_density.rs:27-61)
+// LogPosteriorDensity::update_from_branch (log_posterior_density.rs:27-61);
+// the rss of the device residual comes from the residual operation before it
 void update_lpd(bann_net* t, int b, double others) {
   const Branch& B = t->br[b];
   t->lpd_local[b] = (float)ld_joint_local(t, B);
   t->lpd_outw = (float)ld_joint_out(t, B, others);
-  const double rss = sum_sq(t->residual.data(), t->n);
+  const double rss = t->rss_cur;
   const double le = B.prec[B.epoff];
   t->lpd_rss = (float)(std::log(le) * (t->hp.output_shape + (t->n - 2.0) / 2.0) -
                        le * (rss / 2.0 + 1.0 / t->hp.output_scale));
@@ -316,7 +319,7 @@ int record_perf(bann_net* t) {
   double l = (double)t->lpd_rss + t->lpd_outw;
   for (float v : t->lpd_local) l += v;
   t->lpd.push_back((float)l);
-  t->mse.push_back((float)(sum_sq(t->residual.data(), t->n) / (double)t->n));
+  t->mse.push_back((float)(t->rss_cur / (double)t->n));
   if (t->test_ctx) {
     const int nb = (int)t->br.size();
     const int64_t nt = (int64_t)t->y_test.size();
@@ -638,132 +641,236 @@ extern "C" int bann_net_set_global(bann_net* t, float error_precision, float out
   return BANN_OK;
 }
 
-extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir) {
-  if (!t || !y || !cfg) return BANN_E_ARG;
-  if (cfg->hmc_integration_length < 1 || cfg->chain_length < 0 || cfg->burn_in < 0)
-    return fail(t, BANN_E_ARG, "bad MCMC configuration");
-  if (cfg->hmc_step_size_mode != BANN_STEP_IZMAILOV && cfg->hmc_step_size_mode != BANN_STEP_UNIFORM)
-    return fail(t, BANN_E_ARG, "the driver supports Izmailov and uniform step sizes");
-  t->n = n;
-  const int nb = (int)t->br.size();
-  std::string dir = outdir ? outdir : "";
-  if (!dir.empty() && !mkdir_p(dir + "/models")) return fail(t, BANN_E_ARG, "cannot create " + dir + "/models");
+namespace {
 
-  // initialize_stats (net.rs:158-171): residual = y - bias - sum_b f_b
-  t->residual.assign(y, y + n);
-  for (auto& r : t->residual) r -= t->ob_bias;
-  std::vector<float> pred(n), prev(n), mom;
-  for (int b = 0; b < nb; ++b) {
-    Branch& B = t->br[b];
-    cfg_update_global(t, B);
-    CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
-    const double others = B.ows_reg_sum - B.out_stat();  // from_cfg (branch_struct.rs:26)
-    CKB(bann_predict(t->ctx, b, pred.data()));
-    for (int64_t i = 0; i < n; ++i) t->residual[i] -= pred[i];
-    update_lpd(t, b, others);
+// the per-trajectory draws of one branch update (order: include/bann_net.h)
+struct Draws {
+  std::vector<float> eps, mom;
+  float u = 0.f;
+};
+
+// one branch update of Net::train / train_single_branch (net.rs:261-332): Gibbs
+// draws (unless joint), target = residual + f_b, the HMC trajectory on the
+// device, the residual bookkeeping on the device, global params, output bias
+int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const std::string& dir, Draws& dr) {
+  Branch& B = t->br[b];
+  const int64_t n = t->n;
+  const double kout = t->hp.output_shape, sout = t->hp.output_scale;
+  cfg_update_global(t, B);
+  const double others = B.ows_reg_sum - B.out_stat();  // from_cfg (branch_struct.rs:26)
+  const bool joint = cfg->joint_hmc != 0;
+  if (!joint) {  // net.rs:270-277
+    // sample_error_precision (branch_sampler.rs:190-202): output-layer hyperparameters
+    B.prec[B.epoff] = (float)ridge_posterior(t, kout, sout, t->rss_cur, (double)n);
+    if (!cfg->fixed_param_precisions) {  // sample_param_precisions (173-188)
+      sample_prior_precisions(t, B);
+      const double total = others + B.out_stat();  // add_output_weight_summary_stat_to_global
+      B.prec[B.out_prec_ix()] = (float)(is_lasso(B.prior) ? lasso_posterior(t, kout, sout, total, (double)B.ows_num)
+                                                          : ridge_posterior(t, kout, sout, total, (double)B.ows_num));
+    }
   }
-  {
-    const int rc = record_perf(t);
+  CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
+  CKB(bann_residual_to_target(t->ctx, b));  // net.rs:279-280: fitted to residual + its own prediction
+  int32_t status = 0;
+  if (joint) {  // hmc_step_joint (branch_sampler.rs:1070-1178): random step sizes over [params | precisions]
+    const int64_t PQ = B.P + B.NP;
+    const float f = std::pow((float)PQ, -0.25f) * cfg->hmc_step_size_factor;  // random_step_sizes (654-662)
+    dr.eps.resize(PQ);
+    for (auto& e : dr.eps) e = (float)draw_uniform(t) * f;
+    dr.mom.resize(PQ);
+    for (auto& p : dr.mom) p = (float)draw_normal(t);
+    dr.u = (float)draw_uniform(t);
+    CKB(bann_branch_set_output_stats(t->ctx, b, (float)others, (float)t->g_num));
+    const float hyper[6] = {t->hp.dense_shape, t->hp.dense_scale, t->hp.summary_shape,
+                            t->hp.summary_scale, t->hp.output_shape, t->hp.output_scale};
+    CKB(bann_hmc_step_joint(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error,
+                            BANN_STEP_INJECTED, cfg->hmc_step_size_factor, dr.eps.data(), dr.mom.data(), 0, &dr.u,
+                            hyper, &status, nullptr, nullptr));
+    CKB(bann_branch_get_precisions(t->ctx, b, B.prec.data()));  // to_cfg: the sampled precisions
+  } else {
+    const float* eps = nullptr;
+    int32_t mode = cfg->hmc_step_size_mode;
+    if (mode == BANN_STEP_RANDOM) {  // random_step_sizes (654-681): U(0,1) P^-1/4 c, param_vec order
+      const float f = std::pow((float)B.P, -0.25f) * cfg->hmc_step_size_factor;
+      dr.eps.resize(B.P);
+      for (auto& e : dr.eps) e = (float)draw_uniform(t) * f;
+      eps = dr.eps.data();
+      mode = BANN_STEP_INJECTED;
+    }
+    dr.mom.resize(B.P);
+    for (auto& p : dr.mom) p = (float)draw_normal(t);
+    dr.u = (float)draw_uniform(t);
+    CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
+                      cfg->hmc_step_size_factor, eps, dr.mom.data(), 0, &dr.u, &status, nullptr, nullptr, nullptr));
+  }
+  if (traj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
+    std::string line;
+    int rc = traj_line(t, b, line);
+    if (!rc) rc = append_text(t, dir + "/traj", line);
     if (rc) return rc;
   }
-  const bool trace = cfg->trace && !dir.empty(), traj = cfg->trajectories && !dir.empty();
+  ++t->ns;  // TrainingStats::add_hmc_step_result (train_stats.rs:46-53)
+  if (status == BANN_ACCEPTED) ++t->nacc;
+  if (status == BANN_REJECTED_EARLY) ++t->nearly;
+  CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
+  // net.rs:292-300: residual = target - f_b(final) (accepted: y_pred; rejected: prev_pred)
+  double sr = 0.0;
+  CKB(bann_residual_from_target(t->ctx, b, &sr, &t->rss_cur));
+  if (status == BANN_ACCEPTED) update_lpd(t, b, others);
+  // to_cfg + GlobalParams::update_from_branch_cfg (net.rs:303-305, params.rs:41-56)
+  B.ows_reg_sum = (float)(others + B.out_stat());
+  if (!(B.prec[B.epoff] >= 0.f) || !(B.prec[B.out_prec_ix()] >= 0.f) || !(B.ows_reg_sum >= 0.f))
+    return fail(t, BANN_E_STATE, "invalid global parameter after branch update (params.rs:42-54)");
+  t->g_eprec = B.prec[B.epoff];
+  t->g_oprec = B.prec[B.out_prec_ix()];
+  t->g_reg_sum = B.ows_reg_sum;
+  // output bias (net.rs:319-332): residual += bias, draw, residual -= bias
+  t->ob_eprec = t->g_eprec;
+  CKB(bann_residual_shift(t->ctx, t->ob_bias, &sr, nullptr));
+  if (cfg->sampled_output_bias) {
+    // sample_prior_precision passes the prior SHAPE as the scale (net.rs:61-66)
+    const double bsq = (double)t->ob_bias * t->ob_bias;
+    t->ob_prec = (float)draw_gamma(t, kout + 0.5, 2.0 * kout / (2.0 + kout * bsq));
+    const double den = (double)n * t->ob_eprec + t->ob_prec;  // sample_bias (47-53)
+    t->ob_bias = (float)(t->ob_eprec / den * sr + std::sqrt(1.0 / den) * draw_normal(t));
+  } else {
+    t->ob_bias = (float)(sr / (double)n);  // set_to_maximum_likelihood (43-45)
+  }
+  CKB(bann_residual_shift(t->ctx, -t->ob_bias, nullptr, &t->rss_cur));
+  return BANN_OK;
+}
+
+// checks + initialize_stats (net.rs:158-171) + the first record / trace / model (net.rs:232-249)
+int train_begin(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const std::string& dir,
+                bool& trace, bool& traj) {
+  if (cfg->hmc_integration_length < 1 || cfg->chain_length < 0 || cfg->burn_in < 0)
+    return fail(t, BANN_E_ARG, "bad MCMC configuration");
+  const int32_t m = cfg->hmc_step_size_mode;
+  if (!cfg->joint_hmc && m != BANN_STEP_IZMAILOV && m != BANN_STEP_UNIFORM && m != BANN_STEP_RANDOM)
+    return fail(t, BANN_E_ARG, "step size mode: Izmailov, uniform or random (StdScaled is unusable in the reference)");
+  if (n != bann_ctx_num_individuals(t->ctx)) return fail(t, BANN_E_SHAPE, "phenotype length differs from the cohort");
+  t->n = n;
+  if (!dir.empty() && !mkdir_p(dir + "/models")) return fail(t, BANN_E_ARG, "cannot create " + dir + "/models");
+  // initialize_stats: residual = y - bias - sum_b f_b on the device (one packed forward for stale rows)
+  for (auto& B : t->br) cfg_update_global(t, B);
+  CKB(bann_residual_init(t->ctx, y, t->ob_bias, nullptr, &t->rss_cur));
+  for (int b = 0; b < (int)t->br.size(); ++b) {
+    const Branch& B = t->br[b];
+    update_lpd(t, b, B.ows_reg_sum - B.out_stat());
+  }
+  int rc = record_perf(t);
+  if (rc) return rc;
+  trace = cfg->trace && !dir.empty();
+  traj = cfg->trajectories && !dir.empty();
   if (trace) {  // File::create (net.rs:213-215): a fresh trace, the initial cfgs first (241-244)
     std::remove((dir + "/trace").c_str());
-    const int rc = append_text(t, dir + "/trace", trace_line(t));
+    rc = append_text(t, dir + "/trace", trace_line(t));
     if (rc) return rc;
   }
   CKB(bann_set_trajectory_recording(t->ctx, traj ? 1 : 0));
-  if (!dir.empty() && cfg->burn_in == 0) {
-    const int rc = write_file(t, dir + "/models/0.bin");
-    if (rc) return rc;
-  }
+  if (!dir.empty() && cfg->burn_in == 0) return write_file(t, dir + "/models/0.bin");
+  return BANN_OK;
+}
 
+// record_perf, trace line, model file after a sweep (net.rs:336-353)
+int train_record(bann_net* t, int chain_ix, const bann_mcmc_cfg* cfg, const std::string& dir, bool trace) {
+  int rc = record_perf(t);
+  if (rc) return rc;
+  if (trace && (rc = append_text(t, dir + "/trace", trace_line(t)))) return rc;
+  if (!dir.empty() && chain_ix >= cfg->burn_in) return write_file(t, dir + "/models/" + std::to_string(chain_ix) + ".bin");
+  return BANN_OK;
+}
+
+}  // namespace
+
+extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir) {
+  if (!t || !y || !cfg) return BANN_E_ARG;
+  const std::string dir = outdir ? outdir : "";
+  bool trace = false, traj = false;
+  int rc = train_begin(t, y, n, cfg, dir, trace, traj);
+  if (rc) return rc;
+  const int nb = (int)t->br.size();
   std::vector<int> order(nb);
   for (int b = 0; b < nb; ++b) order[b] = b;
-  double kout = t->hp.output_shape, sout = t->hp.output_scale;
+  Draws dr;
   for (int chain_ix = 1; chain_ix <= cfg->chain_length; ++chain_ix) {
     for (int i = nb - 1; i >= 1; --i) {  // branch_ixs.shuffle (net.rs:257)
       const int j = std::min(i, (int)std::floor(draw_uniform(t) * (i + 1)));
       std::swap(order[i], order[j]);
     }
-    for (int b : order) {
-      Branch& B = t->br[b];
-      cfg_update_global(t, B);
-      const double others = B.ows_reg_sum - B.out_stat();
-      // sample_error_precision (branch_sampler.rs:190-202): output-layer hyperparameters
-      B.prec[B.epoff] = (float)ridge_posterior(t, kout, sout, sum_sq(t->residual.data(), n), (double)n);
-      if (!cfg->fixed_param_precisions) {  // sample_param_precisions (173-188)
-        sample_prior_precisions(t, B);
-        const double total = others + B.out_stat();  // add_output_weight_summary_stat_to_global
-        B.prec[B.out_prec_ix()] = (float)(is_lasso(B.prior) ? lasso_posterior(t, kout, sout, total, (double)B.ows_num)
-                                                            : ridge_posterior(t, kout, sout, total, (double)B.ows_num));
-      }
-      CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
-      // net.rs:279-280: the branch is fitted to residual + its own prediction
-      CKB(bann_predict(t->ctx, b, prev.data()));
-      for (int64_t i = 0; i < n; ++i) t->residual[i] += prev[i];
-      CKB(bann_branch_set_target(t->ctx, b, t->residual.data()));
-      mom.resize(B.P);
-      for (auto& p : mom) p = (float)draw_normal(t);
-      const float u = (float)draw_uniform(t);
-      int32_t status = 0;
-      CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error,
-                        cfg->hmc_step_size_mode, cfg->hmc_step_size_factor, nullptr, mom.data(), 0, &u, &status,
-                        nullptr, nullptr, nullptr));
-      if (traj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
-        std::string line;
-        int rc = traj_line(t, b, line);
-        if (!rc) rc = append_text(t, dir + "/traj", line);
-        if (rc) return rc;
-      }
-      ++t->ns;  // TrainingStats::add_hmc_step_result (train_stats.rs:46-53)
-      if (status == BANN_ACCEPTED) ++t->nacc;
-      if (status == BANN_REJECTED_EARLY) ++t->nearly;
-      CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
-      if (status == BANN_ACCEPTED) {  // net.rs:292-300
-        CKB(bann_predict(t->ctx, b, pred.data()));
-        for (int64_t i = 0; i < n; ++i) t->residual[i] -= pred[i];
-        update_lpd(t, b, others);
-      } else {
-        for (int64_t i = 0; i < n; ++i) t->residual[i] -= prev[i];
-      }
-      // to_cfg + GlobalParams::update_from_branch_cfg (net.rs:303-305, params.rs:41-56)
-      B.ows_reg_sum = (float)(others + B.out_stat());
-      if (!(B.prec[B.epoff] >= 0.f) || !(B.prec[B.out_prec_ix()] >= 0.f) || !(B.ows_reg_sum >= 0.f))
-        return fail(t, BANN_E_STATE, "invalid global parameter after branch update (params.rs:42-54)");
-      t->g_eprec = B.prec[B.epoff];
-      t->g_oprec = B.prec[B.out_prec_ix()];
-      t->g_reg_sum = B.ows_reg_sum;
-      // output bias (net.rs:319-332)
-      t->ob_eprec = t->g_eprec;
-      double sr = 0.0;
-      for (int64_t i = 0; i < n; ++i) sr += (double)(t->residual[i] += t->ob_bias);
-      if (cfg->sampled_output_bias) {
-        // sample_prior_precision passes the prior SHAPE as the scale (net.rs:61-66)
-        const double bsq = (double)t->ob_bias * t->ob_bias;
-        t->ob_prec = (float)draw_gamma(t, kout + 0.5, 2.0 * kout / (2.0 + kout * bsq));
-        const double den = (double)n * t->ob_eprec + t->ob_prec;  // sample_bias (47-53)
-        t->ob_bias = (float)(t->ob_eprec / den * sr + std::sqrt(1.0 / den) * draw_normal(t));
-      } else {
-        t->ob_bias = (float)(sr / (double)n);  // set_to_maximum_likelihood (43-45)
-      }
-      for (int64_t i = 0; i < n; ++i) t->residual[i] -= t->ob_bias;
-    }
-    {
-      const int rc = record_perf(t);
-      if (rc) return rc;
-    }
-    if (trace) {
-      const int rc = append_text(t, dir + "/trace", trace_line(t));
-      if (rc) return rc;
-    }
-    if (!dir.empty() && chain_ix >= cfg->burn_in) {
-      const int rc = write_file(t, dir + "/models/" + std::to_string(chain_ix) + ".bin");
-      if (rc) return rc;
-    }
+    for (int b : order)
+      if ((rc = update_branch(t, b, cfg, traj, dir, dr))) return rc;
+    if ((rc = train_record(t, chain_ix, cfg, dir, trace))) return rc;
   }
   CKB(bann_set_trajectory_recording(t->ctx, 0));
   if (!dir.empty()) return write_training_stats(t, dir);
+  return BANN_OK;
+}
+
+extern "C" int bann_net_train_single_branch(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg,
+                                            const char* outdir) {
+  if (!t || !y || !cfg) return BANN_E_ARG;
+  const std::string dir = outdir ? outdir : "";
+  bool trace = false, traj = false;
+  int rc = train_begin(t, y, n, cfg, dir, trace, traj);
+  if (rc) return rc;
+  Draws dr;
+  for (int chain_ix = 1; chain_ix <= cfg->chain_length; ++chain_ix) {  // net.rs:412-502: branch 0 every time
+    if ((rc = update_branch(t, 0, cfg, traj, dir, dr))) return rc;
+    if ((rc = train_record(t, chain_ix, cfg, dir, trace))) return rc;
+  }
+  CKB(bann_set_trajectory_recording(t->ctx, 0));
+  if (!dir.empty()) return write_training_stats(t, dir);
+  return BANN_OK;
+}
+
+extern "C" int bann_net_perturb(bann_net* t, int32_t has_params, float params_by, int32_t has_precisions,
+                                float precisions_by) {
+  if (!t) return BANN_E_ARG;
+  if (!has_params && !has_precisions) return BANN_OK;
+  for (int b = 0; b < (int)t->br.size(); ++b) {  // BranchCfg::perturb_params / perturb_precisions
+    Branch& B = t->br[b];
+    if (has_params) {
+      for (auto& v : B.params) v += params_by;
+      CKB(bann_branch_set_params(t->ctx, b, B.params.data()));
+    }
+    if (has_precisions) {
+      for (auto& v : B.prec) v += precisions_by;
+      CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
+    }
+  }
+  return BANN_OK;
+}
+
+extern "C" int bann_net_predict(bann_net* t, bann_ctx* ctx, float* y_hat) {
+  if (!t || !y_hat) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  const int nb = (int)t->br.size();
+  if (bann_num_branches(c) != nb) return fail(t, BANN_E_SHAPE, "context branch count differs from the net");
+  for (int b = 0; b < nb; ++b) {
+    int32_t m = 0, L = 0, w[BANN_NET_MAXL] = {0};
+    if (bann_branch_info(c, b, &m, &L, w, BANN_NET_MAXL, nullptr, nullptr) != BANN_OK || m != t->br[b].m ||
+        L != t->br[b].L || L > BANN_NET_MAXL || !std::equal(w, w + L, t->br[b].widths.begin()))
+      return fail(t, BANN_E_SHAPE, "context branches differ from the net's");
+  }
+  const int64_t nt = bann_ctx_num_individuals(c);
+  if (nt <= 0) return fail(t, BANN_E_STATE, "context has no cohort");
+  std::vector<int32_t> all(nb);
+  for (int b = 0; b < nb; ++b) {
+    all[b] = b;
+    if (c != t->ctx) {
+      const int rc = bann_branch_set_params(c, b, t->br[b].params.data());
+      if (rc < 0) return fail(t, rc, std::string("predict context: ") + bann_last_error(c));
+    }
+  }
+  std::vector<float> preds((size_t)nb * nt);
+  const int rc = bann_predict_many(c, all.data(), nb, preds.data());
+  if (rc < 0) return fail(t, rc, std::string("predict: ") + bann_last_error(c));
+  for (int64_t i = 0; i < nt; ++i) {  // y_hat = 0 + bias, then += f_b in branch order (f32, net.rs:546-557)
+    float v = 0.f + t->ob_bias;
+    for (int b = 0; b < nb; ++b) v += preds[(size_t)b * nt + i];
+    y_hat[i] = v;
+  }
   return BANN_OK;
 }
 
@@ -775,11 +882,13 @@ extern "C" int bann_net_set_test_data(bann_net* t, bann_ctx* test_ctx, const flo
     return BANN_OK;
   }
   if (!y_test || n_test <= 0) return fail(t, BANN_E_ARG, "null or empty test targets");
+  if (n_test != bann_ctx_num_individuals(test_ctx))
+    return fail(t, BANN_E_SHAPE, "n_test differs from the test context's cohort size");
   if (bann_num_branches(test_ctx) != (int)t->br.size()) return fail(t, BANN_E_SHAPE, "test context branch count");
   for (int b = 0; b < (int)t->br.size(); ++b) {
-    int32_t m = 0, L = 0, w[8] = {0};
-    if (bann_branch_info(test_ctx, b, &m, &L, w, 8, nullptr, nullptr) != BANN_OK || m != t->br[b].m ||
-        L != t->br[b].L || !std::equal(w, w + L, t->br[b].widths.begin()))
+    int32_t m = 0, L = 0, w[BANN_NET_MAXL] = {0};
+    if (bann_branch_info(test_ctx, b, &m, &L, w, BANN_NET_MAXL, nullptr, nullptr) != BANN_OK || m != t->br[b].m ||
+        L != t->br[b].L || L > BANN_NET_MAXL || !std::equal(w, w + L, t->br[b].widths.begin()))
       return fail(t, BANN_E_SHAPE, "test context branches differ from the training branches");
   }
   t->test_ctx = test_ctx;
@@ -821,9 +930,9 @@ extern "C" int bann_net_records(const bann_net* t, float* mse_train, float* lpd,
 
 extern "C" int bann_net_residual(const bann_net* t, float* out) {
   if (!t || !out) return BANN_E_ARG;
-  if ((int64_t)t->residual.size() != t->n || t->n == 0) return BANN_E_STATE;
-  std::copy(t->residual.begin(), t->residual.end(), out);
-  return BANN_OK;
+  if (t->n == 0) return BANN_E_STATE;
+  const int rc = bann_residual_get(t->ctx, out);
+  return rc < 0 ? rc : BANN_OK;
 }
 
 extern "C" int bann_net_save(const bann_net* t, const char* path) {

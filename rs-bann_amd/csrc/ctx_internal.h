@@ -121,6 +121,21 @@ struct bann_ctx {
   double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)
   double* d_netpart = nullptr; // network mode: rss block partials
   int32_t netrss_cap = 0;
+  double* d_ar64 = nullptr;    // RCCL all-reduce of host f64 vectors (the network -H trace): reused device buffer
+  int64_t ar64_cap = 0;
+  // the network residual on the device (bann_residual.hip): n floats, reduction scratch, pinned (sum, sum sq)
+  float* d_res = nullptr;
+  double* d_res_part = nullptr;
+  double* h_res_stat = nullptr;
+  // pred_ok[b]: the prediction row of branch b is f_b(theta_b) at the current parameters
+  std::vector<char> pred_ok;
+  // in-trajectory launch timing (bann_set_launch_timing): HIP events around every
+  // gradient and update launch of the leapfrog sessions, resolved at bann_leapfrog_end
+  bool tm_on = false;
+  std::vector<hipEvent_t> tm_pool;
+  std::vector<std::pair<int32_t, int32_t>> tm_marks;  // (event index, kind: 0 before grad, 1 after grad, 2 after update)
+  double tm_grad_ms = 0.0, tm_upd_ms = 0.0;
+  int32_t tm_grad_n = 0, tm_upd_n = 0;
   // trajectory recording (mcmc_cfg.trajectories, trajectory.rs): per branch of the last bann_hmc_step
   bool rec_on = false;
   struct Rec {
@@ -167,9 +182,13 @@ bool check_branch(const bann_ctx* ctx, int32_t b);
 int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent);
 void free_plan(Plan& p);
 int run_grad(bann_ctx* ctx, const Plan& p, int write_pred);
+int run_forward(bann_ctx* ctx, const Plan& p);  // predictions only
 void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step);
 int ensure_htrace(bann_ctx* ctx, int32_t L);
 int alloc_genotypes(bann_ctx* ctx, int64_t n, int64_t M);   // the 2-bit genotype image of n x M
 int64_t stage_markers(int64_t bytes_per_marker, int64_t M);  // markers per ~256 MiB staging block
+int ensure_predictions(bann_ctx* ctx, const int32_t* branches, int32_t nb);  // bann_residual.hip
+void launch_residual_sub(float* r, const float* d, int64_t n, hipStream_t s);
+void mark_predictions(bann_ctx* ctx, const Plan& p, bool current);
 int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
                  const float* eps, const float* momentum, uint64_t seed, const float* u);

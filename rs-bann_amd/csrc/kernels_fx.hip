@@ -758,6 +758,189 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 }
 
 // ===========================================================================
+// Forward-only fx pass: f_b(theta) of every individual (forward_feed,
+// branch_sampler.rs:743-782, at the output neuron), no target, no backward.
+// Network-joint HMC needs the summed branch outputs before any branch can form
+// its output error, so each of its leapfrog steps starts with this pass; the
+// prediction paths (bann_predict*, stale rows before a target rebuild) use it
+// too.  Same tiles, work items, W0 digits and head as k_fused_grad_fx; the
+// stream runs two tiles ahead in the wave's two slots, the refill of a slot is
+// issued once the forward has read it (the head's prediction store first, so
+// the counted wait at the top never waits on a piece younger than the tile).
+// ===========================================================================
+template <int NL, int ACT, int NCH>
+__global__ void __launch_bounds__(64 * FX_WAVES, 2)
+    k_forward_fx(DevState st, const GradItem* __restrict__ items) {
+  constexpr int NH = NL - 1;
+  constexpr int NW = FX_WAVES;
+  __shared__ __attribute__((aligned(16))) char s_x[NW][2][FX_SLOT];
+  __shared__ __attribute__((aligned(16))) char s_w0[8 * 1024];
+  __shared__ __attribute__((aligned(16))) float s_hw[NL][20];
+
+  const GradItem it = items[blockIdx.x];
+  const int b = it.branch;
+  const BranchDev& bd = st.br[b];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int nch = NCH ? NCH : bd.nchunks;
+  const int64_t n = st.n;
+  const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
+
+  const float* th = st.theta + bd.p_off;
+  for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (r < 16) {
+      const int j = r >> 2, k = r & 3;
+      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+    } else {
+      const int k = r - 16;
+      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+    }
+    s_hw[l][r] = v;
+  }
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
+  float zscale = st.fc[b].scale[g];
+  for (int c = wave; c < nch; c += NW)
+    *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
+        *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(zscale));
+  __syncthreads();
+  float uWm[NL][4][4], uB[NH][4];  // head weights W_l[j][k] (l >= 1; output layer: k = 0) and biases, scalar
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        uWm[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l][4 * j + k]) : 0.f;
+    if (l < NH)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l][16 + k]);
+  }
+
+  const int gsw = g & 1;
+  const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
+  const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
+  const int iota = 4 * i16 + g;
+  float* predb = st.pred + bd.y_off;
+  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
+  const int64_t tile_bytes = (int64_t)nch * 1024;
+  auto issue_chunk = [&](int tt, int sl, int c) {
+    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
+  };
+
+  int tt = tb + wave, sl = 0;
+  if (tt < te) {
+    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
+    if (tt + NW < te)
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
+  }
+  for (; tt < te; tt += NW, sl ^= 1) {
+    const bool more = tt + NW < te, more2 = tt + 2 * NW < te;
+    vm_wait(more ? nch : 0);  // this tile has landed; the next tile's nch pieces may fly
+    const char* xs = &s_x[wave][sl][0];
+    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+    {
+      constexpr int FD = 2;
+      v4u Xq[FD];
+      v4i Aq[FD];
+#pragma unroll
+      for (int c = 0; c < FD; ++c) {
+        Xq[c] = v4u{0u, 0u, 0u, 0u};
+        Aq[c] = v4i{0, 0, 0, 0};
+        if (NCH != 0 || c < nch) {
+          Xq[c] = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+          Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (NCH == 0 && c >= nch) continue;
+        const v4u Xc = Xq[c % FD];
+        const v4i Ac = Aq[c % FD];
+        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {
+          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
+          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
+        }
+        const v4i B0 = (v4i)(Xc & 0x03030303u);
+        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
+        const v4i B2 = (v4i)(Xc & 0x30303030u);
+        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
+        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B0, facc[0], 0, 0, 0);
+        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B1, facc[1], 0, 0, 0);
+        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B2, facc[2], 0, 0, 0);
+        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
+    swap32(z0, z2);
+    swap32(z1, z3);
+    swap16(z0, z1);
+    swap16(z2, z3);
+    float a[4];
+    a[0] = act_h_t<ACT>(z0 + uB[0][0]);
+    a[1] = act_h_t<ACT>(z1 + uB[0][1]);
+    a[2] = act_h_t<ACT>(z2 + uB[0][2]);
+    a[3] = act_h_t<ACT>(z3 + uB[0][3]);
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+      float an[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float s = uB[l][k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s = fmaf(a[j], uWm[l][j][k], s);
+        an[k] = act_h_t<ACT>(s);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = an[k];
+    }
+    float out = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out = fmaf(a[j], uWm[NL - 1][j][0], out);
+    const int64_t row = 64 * (int64_t)tt + iota;
+    if (row < n) predb[row] = out;
+    // every read of this slot has returned (the MFMAs consumed them): refill it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more2)
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + 2 * NW, sl, c);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NL, int NCH>
+static void launch_fwd_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
+  switch (act) {
+    case 0: hipLaunchKernelGGL((k_forward_fx<NL, 0, NCH>), grid, block, 0, s, st, items); break;
+    case 1: hipLaunchKernelGGL((k_forward_fx<NL, 1, NCH>), grid, block, 0, s, st, items); break;
+    case 2: hipLaunchKernelGGL((k_forward_fx<NL, 2, NCH>), grid, block, 0, s, st, items); break;
+    case 3: hipLaunchKernelGGL((k_forward_fx<NL, 3, NCH>), grid, block, 0, s, st, items); break;
+    default: hipLaunchKernelGGL((k_forward_fx<NL, 4, NCH>), grid, block, 0, s, st, items); break;
+  }
+}
+
+void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act, int full8,
+                       hipStream_t s) {
+  if (nitems <= 0) return;
+  switch (L * 2 + (full8 ? 1 : 0)) {
+    case 4: launch_fwd_nl<2, 0>(st, items, nitems, act, s); break;
+    case 5: launch_fwd_nl<2, 8>(st, items, nitems, act, s); break;
+    case 6: launch_fwd_nl<3, 0>(st, items, nitems, act, s); break;
+    case 7: launch_fwd_nl<3, 8>(st, items, nitems, act, s); break;
+    case 8: launch_fwd_nl<4, 0>(st, items, nitems, act, s); break;
+    case 9: launch_fwd_nl<4, 8>(st, items, nitems, act, s); break;
+    default: break;
+  }
+}
+
+// ===========================================================================
 // "fxl": the fx scheme for branches of 9 .. 64 marker chunks (m_b <= 4096, e.g.
 // BASELINE config C2's 2 000-SNP branches).
 //

@@ -1,0 +1,37 @@
+"""bench.py's own N-rank launch (CPU, gloo): `python bench.py --gpus 2` run
+directly starts torch.distributed.run as a child process (no exec, nothing on
+the GPU in the parent); with --check-launch every rank takes its
+marker-balanced shard and runs the library's residual exchange step
+(bann_residual_update_host, the exchange bann_exchange_residual performs for a
+callback communicator), and rank 0's JSON line comes back through the parent."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args):
+    env = dict(os.environ, BANN_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout   # ONE JSON line, rank 0's
+    return json.loads(lines[0]), p.stderr
+
+
+def test_bench_launches_two_ranks():
+    out, err = _run(["--gpus", "2", "--check-launch"])
+    assert "launching 2 ranks" in err
+    assert out["n_gpus"] == 2 and out["parallelism"] == "branch-shard x2"
+    assert out["ranks"] == [0, 1]
+    assert out["shards"] == [[0, 500], [500, 1000]]
+    assert out["exchange_max_err"] == 0.0
+
+
+def test_bench_single_rank_runs_in_process():
+    out, err = _run(["--gpus", "1", "--check-launch"])
+    assert "launching" not in err
+    assert out["n_gpus"] == 1 and out["ranks"] == [0] and out["shards"] == [[0, 1000]]

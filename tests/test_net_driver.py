@@ -56,19 +56,33 @@ def rel(a, b):
     return abs(a - b) / max(abs(b), 1e-12)
 
 
-@pytest.mark.parametrize("prior,sampled_bias", [("ridge_ard", False), ("ridge_ard", True), ("lasso_base", False),
-                                                ("lasso_ard", True)])
-def test_train_matches_oracle(prior, sampled_bias):
+@pytest.mark.parametrize("prior,opts", [
+    ("ridge_ard", {}), ("ridge_ard", dict(sampled_output_bias=True)), ("lasso_base", {}),
+    ("lasso_ard", dict(sampled_output_bias=True)),
+    # MCMCCfg::joint_hmc: hmc_step_joint, no Gibbs draws (net.rs:270-290)
+    ("ridge_ard", dict(joint_hmc=True, factor=0.5)), ("lasso_base", dict(joint_hmc=True, factor=0.5)),
+    # StepSizeMode::Random (branch_sampler.rs:654-681, 1212-1217)
+    ("ridge_base", dict(step_mode="random")),
+    # Net::train_single_branch (net.rs:360-507)
+    ("ridge_ard", dict(single_branch=True)),
+])
+def test_train_matches_oracle(prior, opts):
     from bann import MCMCConfig, Net
     ctx, branches, X, y = build(prior)
     hp = O.Hyper()
     net = Net(ctx, (hp.dense, hp.summary, hp.output))
     d_dev, d_ora = NO.Draws(11), NO.Draws(11)
     net.set_rng(d_dev.uniform, d_dev.normal, d_dev.gamma)
-    cfg = MCMCConfig(hmc_integration_length=10, chain_length=3, sampled_output_bias=sampled_bias)
-    net.train(y, cfg)
+    sampled_bias = opts.get("sampled_output_bias", False)
+    factor = opts.get("factor", 1.0)
+    single = opts.get("single_branch", False)
+    cfg = MCMCConfig(hmc_integration_length=10, chain_length=3, sampled_output_bias=sampled_bias,
+                     hmc_step_size_factor=factor, hmc_step_size_mode=opts.get("step_mode", "izmailov"),
+                     joint_hmc=opts.get("joint_hmc", False))
+    (net.train_single_branch if single else net.train)(y, cfg)
     ora = NO.NetOracle(branches, X, hp)
-    ora.train(y.astype(np.float64), d_ora, 3, 10, sampled_output_bias=sampled_bias)
+    ora.train(y.astype(np.float64), d_ora, 3, 10, factor=factor, step_mode=opts.get("step_mode", "izmailov"),
+              sampled_output_bias=sampled_bias, joint_hmc=opts.get("joint_hmc", False), single_branch=single)
     assert d_dev.uniform() == d_ora.uniform(), "draw streams diverged (different number of draws)"
     s = net.summary()
     assert (s["num_samples"], s["num_accepted"], s["num_early_rejected"]) == (ora.ns, ora.nacc, ora.nearly)
@@ -267,3 +281,59 @@ def test_trajectory_recording_matches_oracle_hmc():
         assert norm_rel(tr["params"][k], th) < 1e-5, k
         assert norm_rel(tr["ldg"][k], g) < 1e-5, k
     ctx.close()
+
+
+def test_perturb_predict_and_test_data_checks():
+    """Net::perturb (net.rs:187-199: + by to every param / precision), Net::predict
+    (net.rs:545-559: bias + sum_b f_b, on the training cohort and on another
+    cohort with the same branches), and bann_net_set_test_data refusing a
+    y_test whose length is not the test cohort's."""
+    from bann import BannContext, BannError, MCMCConfig, Net
+    ctx, branches, X, y = build("ridge_ard", seed=13)
+    net = Net(ctx, seed=2)
+    net.train(y, MCMCConfig(hmc_integration_length=5, chain_length=2, hmc_step_size_factor=0.3))
+    p0 = [ctx.get_params(b) for b in range(3)]
+    q0 = [ctx.get_precisions(b) for b in range(3)]
+    net.perturb(params_by=0.01)
+    for b in range(3):
+        assert np.array_equal(ctx.get_params(b), p0[b] + np.float32(0.01))
+        assert np.array_equal(ctx.get_precisions(b), q0[b])
+    net.perturb(precisions_by=0.5)
+    for b in range(3):
+        assert np.array_equal(ctx.get_precisions(b), q0[b] + np.float32(0.5))
+    bias = net.summary()["output_bias"]
+    f = np.zeros(y.size)
+    for b in range(3):
+        bw, bb = O.load_param_vec(ctx.get_params(b).astype(np.float64), branches[b].num_markers,
+                                  branches[b].layer_widths)
+        br = branches[b].copy()
+        br.weights, br.biases = bw, bb
+        f += O.predict(br, X[b])
+    yh = net.predict()
+    assert norm_rel(yh, f + bias) < 1e-5
+    # another cohort with the same branches
+    rng = np.random.default_rng(5)
+    ms = (40, 64, 30)
+    gt = O.synthetic_genotypes(rng, 250, sum(ms))
+    tctx = BannContext(0)
+    tctx.upload_genotypes(gt)
+    off = 0
+    for m, br in zip(ms, branches):
+        tctx.add_branch(np.arange(off, off + m, dtype=np.int32), br.layer_widths, "tanh", "ridge_ard")
+        off += m
+    tctx.finalize()
+    mu, sd = tctx.genotype_stats()
+    ft, off = np.zeros(250), 0
+    for b, m in enumerate(ms):
+        s_ = np.arange(off, off + m)
+        off += m
+        bw, bb = O.load_param_vec(ctx.get_params(b).astype(np.float64), m, branches[b].layer_widths)
+        br = branches[b].copy()
+        br.weights, br.biases = bw, bb
+        ft += O.predict(br, x_std(gt[s_], mu[s_], sd[s_]))
+    assert norm_rel(net.predict(tctx), ft + bias) < 1e-5
+    with pytest.raises(BannError):   # n_test must be the test cohort's size (it sizes the prediction buffer)
+        net.set_test_data(tctx, np.zeros(100, np.float32))
+    net.set_test_data(tctx, np.zeros(250, np.float32))
+    for o in (net, ctx, tctx):
+        o.close()

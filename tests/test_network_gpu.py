@@ -93,7 +93,7 @@ def _free_port():
     return p
 
 
-def _rank_worker(rank, world, port, out):
+def _rank_worker(rank, world, port, out, u=0.5):
     import torch.distributed as dist
     from bann.distributed import TorchAllreduce, shard_ranges
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -108,20 +108,23 @@ def _rank_worker(rank, world, port, out):
     if world > 1:
         ctx.comm_callback(TorchAllreduce(dist), world, rank)
     res = ctx.network_hmc_step(y, L, bias=-0.1, lambda_e=0.8, eps=np.concatenate(eps[lo:hi]),
-                               momentum=np.concatenate(mom[lo:hi]), u=0.5)
+                               momentum=np.concatenate(mom[lo:hi]), u=u, seed=17)
     out[rank] = dict(status=res["status"], trace=res["trace"],
                      params=[ctx.get_params(i) for i in range(hi - lo)], lo=lo)
     ctx.close()
     dist.destroy_process_group()
 
 
-def test_network_hmc_two_ranks_match_one():
+@pytest.mark.parametrize("u", [0.5, None])
+def test_network_hmc_two_ranks_match_one(u):
+    """u = None: the library draws the Metropolis uniform on rank 0 and shares it
+    through the -H all-reduce, so both ranks take the one-rank decision."""
     import torch.multiprocessing as mp
     results = {}
     for world in (1, 2):
         mgr = mp.Manager()
         out = mgr.dict()
-        mp.spawn(_rank_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        mp.spawn(_rank_worker, args=(world, _free_port(), out, u), nprocs=world, join=True)
         results[world] = dict(out)
     one, two = results[1][0], results[2]
     assert two[0]["status"] == two[1]["status"] == one["status"]
