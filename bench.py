@@ -5,20 +5,24 @@
 One "step" = one full-cohort leapfrog step: a packed gradient evaluation of
 every branch (one fused HIP launch) + the fused momentum/position/-H update
 (one launch).  The timed region is one whole HMC trajectory of K steps for
-every branch: momentum draw + initial gradient, the K steps, the Metropolis
-decision and the residual change of the accepted branches (the bookkeeping of
-net.rs:279-300); value = K / elapsed.  Warmup = one untimed trajectory of W
-steps.  Genotypes are synthetic (generated on the device), resident in HBM as
-int8 before the timed region.
+every branch: momentum draw + initial gradient, the K steps and the Metropolis
+decision; value = K / elapsed.  Each branch runs on its conditional posterior
+given the other branches (the target residual + f_b of net.rs:279-280, built
+on the device).  Warmup = one untimed trajectory of W steps, then the
+roofline's back-to-back launch timing (the GPU clock settles under load).
+Genotypes are synthetic (generated on the device), resident in HBM as 2-bit
+tile images before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W]
   (N > 1: one rank per GPU.  Run directly, bench.py starts the N ranks itself
    -- torch.distributed.run as a CHILD process, before anything touches the GPU
    -- and rank 0's JSON line passes through; under an outer
    torch.distributed.run (WORLD_SIZE set) it is one of the ranks.  The 1k
-   branches are sharded over the ranks, no collective inside a step; the
-   trajectory end all-reduces the n-vector residual change over RCCL.
-   BANN_DIST_BACKEND=gloo rehearses N ranks on one GPU.)
+   branches are sharded over the ranks by marker count; a branch-sampler step
+   needs no collective (branches share no weights), the timed region ends at a
+   barrier and the max over ranks.  --sampler network all-reduces the summed
+   branch outputs over RCCL every step.  BANN_DIST_BACKEND=gloo rehearses N
+   ranks on one GPU.)
 
 Prints ONE JSON line (rank 0).
 """
@@ -199,6 +203,8 @@ def main():
         # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
         # curvature, c = 1 rejects every trajectory; c = 0.1 accepts ~0.9 at L = 100 (tools/gpu_c5sweep.sh)
         args.step_factor = {"c5": 0.1, "c3def": 0.02}.get(args.config, 1.0)
+        if args.sampler == "network":   # the joint state's energy error sums over all 1000 branches
+            args.step_factor = {"c3": 0.12}.get(args.config, 0.1 * args.step_factor)
     heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
     if args.cpu_sample_branches is None:
         args.cpu_sample_branches = 4 if heavy else 96
@@ -290,12 +296,17 @@ def main():
 
     def trajectory(L, seed):
         """one HMC trajectory of L leapfrog steps.  branch sampler: every branch of
-        this rank (momentum draw + initial gradient, L fused steps, Metropolis),
-        then the residual change of the accepted branches summed over the ranks into
-        the device residual (bann_exchange_residual_device) and every branch target
-        rebuilt from it for the next trajectory (bann_rebuild_targets).  network
-        sampler: one HMC state over all branches of all ranks, the summed outputs
-        all-reduced every step (bann_network_hmc_step)."""
+        this rank (momentum draw + initial gradient, L fused steps, Metropolis) on
+        its conditional posterior given the other branches at the sweep start (the
+        target y_b = residual + f_b of net.rs:279-280, built on the device).  The
+        targets are NOT rebuilt between trajectories: a simultaneous (Jacobi)
+        update of 1000 overlapping branches (2M parameters, n = 50k) overshoots the
+        residual -- measured: ||r||^2 +70 % after one trajectory and every later
+        trajectory rejected early (tools/diag_c3.py) -- so the
+        residual bookkeeping of a sweep belongs to the sequential driver
+        (--sampler sequential, the reference's Gauss-Seidel order) and the
+        network sampler.  network sampler: one HMC state over all branches of all
+        ranks, the summed outputs all-reduced every step (bann_network_hmc_step)."""
         if args.sampler == "sequential":   # one sweep: every branch one L-step trajectory, in shuffled order
             net.train(y_net, MCMCConfig(hmc_step_size_factor=args.step_factor, hmc_integration_length=L,
                                         chain_length=1, burn_in=1))
@@ -309,8 +320,6 @@ def main():
         ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
         ctx.leapfrog_steps(L)
         status, acc = ctx.leapfrog_end()
-        ctx.exchange_residual_device()
-        ctx.rebuild_targets(branches)
         return acc
 
     # warmup: a full trajectory of W steps (loads every kernel), then the
@@ -325,9 +334,6 @@ def main():
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99 + rank)
     b2b_grad_ms, b2b_upd_ms = ctx.profile_session(args.profile_iters)
     ctx.leapfrog_end()
-    if args.sampler == "branch":
-        ctx.exchange_residual_device()
-        ctx.rebuild_targets(branches)
     timing = args.sampler == "branch" and not args.no_launch_timing
     if timing:   # HIP events around every gradient / update launch of the timed trajectory
         ctx.launch_timing(reset=True)

@@ -35,7 +35,10 @@ void free_plan(Plan& p) {
   p = Plan{};
 }
 
+void clear_graphs(bann_ctx* ctx);
+
 void refresh_state(bann_ctx* ctx) {
+  clear_graphs(ctx);  // captured kernel arguments hold the old state
   DevState& s = ctx->st;
   s.br = ctx->d_br;
   s.xu2 = ctx->d_xu2;
@@ -429,6 +432,7 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   if (device < 0 || device >= ndev) return BANN_E_ARG;
   bann_ctx* ctx = new bann_ctx();
   ctx->device = device;
+  if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return BANN_E_HIP;
@@ -459,6 +463,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res,
                   ctx->d_res_part};
   for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
+  clear_graphs(ctx);
   comm_destroy(ctx);
   for (void* p : bufs) dfree(p);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
@@ -1238,6 +1243,103 @@ int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t 
   return BANN_OK;
 }
 
+// per-branch outputs of a finished bann_hmc_step (the stream has drained)
+static int hmc_outputs(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, int32_t* status_out,
+                       double* h_trace_out, int32_t* uturn_out, double* log_density_out) {
+  const int stride = ctx->htrace_cap;
+  for (int i = 0; i < nb; ++i) {
+    const int b = branches[i];
+    if (status_out) CK(hipMemcpy(status_out + i, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (uturn_out) CK(hipMemcpy(uturn_out + i, ctx->d_uturn + b, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (log_density_out) CK(hipMemcpy(log_density_out + i, ctx->d_ld + b, sizeof(double), hipMemcpyDeviceToHost));
+    if (h_trace_out)
+      CK(hipMemcpy(h_trace_out + (int64_t)i * (L + 1), ctx->d_htrace + (int64_t)b * stride, (L + 1) * sizeof(double),
+                   hipMemcpyDeviceToHost));
+  }
+  return BANN_OK;
+}
+
+// ---- graph replay of a trajectory's launch sequence (bann_hmc_step) ----
+// The sequential driver runs one small trajectory after another (one branch,
+// L steps of gradient + update launches): the host's launch overhead, not the
+// GPU, paces it.  The sequence of a plan shape is captured once into a HIP
+// graph and replayed; the plan's device arrays live in the context's scratch
+// buffers (fixed addresses), so one graph serves every branch of the same shape.
+// The key holds everything the captured kernel arguments depend on.
+static std::string traj_graph_key(const bann_ctx* ctx, const Plan& p, int32_t L) {
+  std::string k;
+  auto put = [&](int64_t v) { k.append(reinterpret_cast<const char*>(&v), sizeof(v)); };
+  put(L);
+  put(ctx->wide_bf16);
+  put((int64_t)p.all.size());
+  put(p.n_small);
+  put(p.n_large);
+  put(p.max_p);
+  put((int64_t)p.fold.size());
+  put((int64_t)(intptr_t)p.d_all);
+  put((int64_t)(intptr_t)p.d_fold);
+  put((int64_t)(intptr_t)p.d_gx);
+  put((int64_t)(intptr_t)p.d_gxpre);
+  for (const auto& g : p.groups) {
+    put(g.kind), put(g.L), put(g.act), put(g.nw), put(g.full);
+    put((int64_t)g.items.size());
+    put((int64_t)(intptr_t)g.d_items);
+  }
+  for (const auto& g : p.gxg) {
+    put(g.first), put(g.count), put(g.max_splits);
+    for (const auto& ph : g.phases) put(ph.ph), put(ph.l), put(ph.total), put(ph.pre_off);
+  }
+  k.append(reinterpret_cast<const char*>(&ctx->st), sizeof(DevState));  // the kernels' by-value state
+  return k;
+}
+
+void clear_graphs(bann_ctx* ctx) {
+  for (auto& e : ctx->graphs) (void)hipGraphExecDestroy(e.second);
+  ctx->graphs.clear();
+}
+
+// the launches of one trajectory after traj_prepare: initial gradient (f(theta_0) -> pred0),
+// INIT update, L x (gradient, update), restore of the rejected branches' predictions
+static int traj_launches(bann_ctx* ctx, const Plan& p, int32_t L) {
+  int rc = run_grad(ctx, p, 2);
+  if (rc) return rc;
+  run_update(ctx, p, MODE_INIT, 0);
+  for (int k = 1; k <= L; ++k) {
+    rc = run_grad(ctx, p, k == L ? 1 : 0);
+    if (rc) return rc;
+    run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
+  }
+  launch_restore_pred(ctx->st, p.d_all, (int32_t)p.all.size(), ctx->stream);
+  CK(hipGetLastError());
+  return BANN_OK;
+}
+
+static int traj_replay(bann_ctx* ctx, const Plan& p, int32_t L) {
+  const std::string key = traj_graph_key(ctx, p, L);
+  hipGraphExec_t exec = nullptr;
+  for (auto& e : ctx->graphs)
+    if (e.first == key) exec = e.second;
+  if (!exec) {
+    if (ctx->graphs.size() >= 16) clear_graphs(ctx);
+    CK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    const int rc = traj_launches(ctx, p, L);
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(ctx->stream, &g);
+    if (rc) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    CK(ee);
+    const hipError_t ei = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    CK(ei);
+    ctx->graphs.push_back({key, exec});
+  }
+  CK(hipGraphLaunch(exec, ctx->stream));
+  mark_predictions(ctx, p, true);
+  return BANN_OK;
+}
+
 extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
                              int32_t step_mode, float factor, const float* eps, const float* momentum, uint64_t seed,
                              const float* u, int32_t* status_out, double* h_trace_out, int32_t* uturn_out,
@@ -1253,6 +1355,12 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   if (rc) return rc;
   rc = traj_prepare(ctx, p, std::max(L, 1), max_dh, step_mode, factor, eps, momentum, seed, u);
   if (rc) return rc;
+  if (L >= 1 && !ctx->rec_on && ctx->graph_replay) {  // the whole launch sequence as one graph launch
+    rc = traj_replay(ctx, p, L);
+    if (rc) return rc;
+    CK(hipStreamSynchronize(ctx->stream));
+    return hmc_outputs(ctx, branches, nb, L, status_out, h_trace_out, uturn_out, log_density_out);
+  }
   rc = run_grad(ctx, p, L == 0 ? 1 : 2);  // f(theta_0) -> pred0 (restore copy of a rejected branch)
   if (rc) return rc;
   if (L == 0) {  // empty leapfrog loop: accept_or_reject at the initial state accepts
@@ -1311,16 +1419,7 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
       R.steps = steps;
       R.h.resize(steps + 1);
     }
-  for (int i = 0; i < nb; ++i) {
-    const int b = branches[i];
-    if (status_out) CK(hipMemcpy(status_out + i, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (uturn_out) CK(hipMemcpy(uturn_out + i, ctx->d_uturn + b, sizeof(int32_t), hipMemcpyDeviceToHost));
-    if (log_density_out) CK(hipMemcpy(log_density_out + i, ctx->d_ld + b, sizeof(double), hipMemcpyDeviceToHost));
-    if (h_trace_out)
-      CK(hipMemcpy(h_trace_out + (int64_t)i * (L + 1), ctx->d_htrace + (int64_t)b * stride, (L + 1) * sizeof(double),
-                   hipMemcpyDeviceToHost));
-  }
-  return BANN_OK;
+  return hmc_outputs(ctx, branches, nb, L, status_out, h_trace_out, uturn_out, log_density_out);
 }
 
 // hmc_step_joint (branch_sampler.rs:1070-1178): parameters AND precisions
@@ -1523,7 +1622,6 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
 extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   if (!ctx || !ctx->lf_active) return fail(ctx, BANN_E_STATE, "no leapfrog session");
   if (k < 0 || ctx->lf_step + k > ctx->lf_L) return fail(ctx, BANN_E_ARG, "steps beyond the trajectory length");
-  const int32_t nb = (int32_t)ctx->lf.all.size();
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
     tm_mark(ctx, 0);
@@ -1601,7 +1699,6 @@ extern "C" int bann_profile_session(bann_ctx* ctx, int32_t iters, float* grad_ms
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventCreate(&e2));
-  const int32_t nb = (int32_t)ctx->lf.all.size();
   CK(hipEventRecord(e0, ctx->stream));
   for (int i = 0; i < iters; ++i) {
     int rc = run_grad(ctx, ctx->lf, 0);

@@ -144,6 +144,9 @@ struct bann_ctx {
     std::vector<double> h;           // [L + 1]
   };
   std::vector<Rec> rec;  // indexed by branch
+  // captured launch sequences of bann_hmc_step, keyed by plan shape, L and the by-value state
+  bool graph_replay = true;  // BANN_HMC_GRAPH=0: launch from the host every time
+  std::vector<std::pair<std::string, hipGraphExec_t>> graphs;
   // leapfrog session
   Plan lf;
   bool lf_active = false;

@@ -610,27 +610,40 @@ void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb,
 }
 
 // solo-mode fold (build_plan): the nslab partial slabs a solo plan wrote for a
-// branch, summed in slab order into the branch's slab 0; its other slabs and rss
-// partials zeroed, so k_update's fixed-order split reduction sees the same sum
-// grid (parameter blocks of 64, jobs): one thread per parameter, its slabs'
-// loads independent (unrolled), many small blocks so the loads of a few hundred
-// slabs spread over the CUs
-__global__ void __launch_bounds__(64) k_fold_solo(DevState st, const FoldJob* __restrict__ jobs) {
+// branch, summed into the branch's slab 0; its other slabs and rss partials
+// zeroed, so k_update's fixed-order split reduction sees the same sum.
+// grid (parameter blocks of 32, jobs), 256 threads: thread (lane q of 8, param
+// p) adds slabs q, q + 8, ... in order (its loads independent, all in flight),
+// then lane 0 adds the 8 partials in q order -- a fixed order, one round of
+// memory latency instead of nslab / 16 (the single-branch step of the
+// sequential driver: 15 -> ~4 us)
+#define FOLD_Q 8
+__global__ void __launch_bounds__(256) k_fold_solo(DevState st, const FoldJob* __restrict__ jobs) {
+  __shared__ float s_part[FOLD_Q][32];
   const FoldJob j = jobs[blockIdx.y];
   const BranchDev& bd = st.br[j.branch];
   const int P = bd.P;
   float* dst = st.part + bd.part_off;
   const float* src = st.part + j.part;
-  const int i = blockIdx.x * 64 + threadIdx.x;
+  const int q = threadIdx.x >> 5, pl = threadIdx.x & 31;
+  const int i = blockIdx.x * 32 + pl;
+  float v = 0.f;
   if (i < P) {
-    float v = 0.f;
-#pragma unroll 16
-    for (int s = 0; s < j.nslab; ++s) v += src[(int64_t)s * P + i];
-    dst[i] = v;
+#pragma unroll 8
+    for (int s = q; s < j.nslab; s += FOLD_Q) v += src[(int64_t)s * P + i];
+  }
+  s_part[q][pl] = v;
+  __syncthreads();
+  if (q == 0 && i < P) {
+    float t = s_part[0][pl];
+#pragma unroll
+    for (int k = 1; k < FOLD_Q; ++k) t += s_part[k][pl];
+    dst[i] = t;
     for (int s = 1; s < bd.nsplits; ++s) dst[(int64_t)s * P + i] = 0.f;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     double r = 0.0;
+#pragma unroll 16
     for (int s = 0; s < j.nslab; ++s) r += st.rss_part[j.rss + s];
     double* rd = st.rss_part + (int64_t)j.branch * st.max_splits;
     rd[0] = r;
@@ -639,7 +652,7 @@ __global__ void __launch_bounds__(64) k_fold_solo(DevState st, const FoldJob* __
 }
 
 void launch_fold_solo(const DevState& st, const FoldJob* jobs, int32_t njobs, int32_t max_p, hipStream_t s) {
-  if (njobs > 0) hipLaunchKernelGGL(k_fold_solo, dim3((max_p + 63) / 64, njobs), dim3(64), 0, s, st, jobs);
+  if (njobs > 0) hipLaunchKernelGGL(k_fold_solo, dim3((max_p + 31) / 32, njobs), dim3(256), 0, s, st, jobs);
 }
 
 // momentum ~ N(0, 1) (sample_momentum, branch_sampler.rs:594-609): Box-Muller on Philox
