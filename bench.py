@@ -169,6 +169,12 @@ def main():
                          "branch outputs all-reduced every leapfrog step (bann_network_hmc_step); sequential: the "
                          "reference's own sweep order, one branch at a time against the refreshed residual "
                          "(bann_net_train, Net::train net.rs:201-358), one GPU")
+    ap.add_argument("--no-network-check", action="store_true",
+                    help="N > 1: skip the short network-joint trajectory through the library's RCCL communicator "
+                         "that follows the JSON line (stderr)")
+    ap.add_argument("--accept-trajectories", type=int, default=None,
+                    help="untimed trajectories after the timed one whose acceptance is reported beside it "
+                         "(default 4 for --sampler network: one Metropolis decision per trajectory)")
     ap.add_argument("--check-launch", action="store_true",
                     help="no GPU: run the N-rank launch, shard and the library's residual exchange step only (CPU test)")
     args = ap.parse_args()
@@ -270,9 +276,9 @@ def main():
     ctx.synchronize()
     setup_s = time.time() - t_setup
 
-    # the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
-    # all-reduce callback when rehearsing N ranks on one GPU
-    if dist is not None:
+    def library_comm():
+        """the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
+        all-reduce callback when rehearsing N ranks on one GPU"""
         import torch
         if backend == "nccl":
             idt = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local_rank}")
@@ -283,6 +289,9 @@ def main():
         else:
             ctx.comm_callback(TorchAllreduce(dist), world, rank)
         torch.cuda.synchronize()
+
+    if dist is not None and args.sampler == "network":   # the per-step all-reduce needs it in the timed region
+        library_comm()
     branches = list(range(nb))
     y_net = (noise + fsum).astype(np.float32)
 
@@ -363,6 +372,17 @@ def main():
         acc_all, nb_all = float(ta[0]), float(ta[1])
     else:
         acc_all, nb_all = float(acc), float(nb)
+    # acceptance over more (untimed) trajectories: the network sampler takes ONE
+    # Metropolis decision per trajectory, so a single trajectory says 0 or 1
+    n_extra = args.accept_trajectories if args.accept_trajectories is not None else (
+        4 if args.sampler == "network" else 0)
+    accs = [acc / nb]
+    for i in range(n_extra):
+        accs.append(trajectory(args.steps, seed=101 + 7 * i + rank) / nb)
+    if dist is not None and n_extra:
+        ta = torch.tensor(accs, device=dist_dev, dtype=torch.float64)
+        dist.all_reduce(ta)
+        accs = [float(v) / world for v in ta]
 
     workload = (f"{args.config}: {B_total} branches x {m_b} SNPs, n={n}, D=1 W={widths[0]} S={widths[1]}, RidgeARD, "
                 "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else "") +
@@ -459,12 +479,36 @@ def main():
                          "alg_bytes_basis": "2-bit genotypes (n*m_b/4) + 4n target bytes per branch", "update_kernel_ms": upd_ms},
             "cpu_baseline": cpu,
             "accept_rate": acc_all / nb_all,
+            **({"accept_rate_trajectories": {"trajectories": len(accs), "rate": float(np.mean(accs))}}
+               if n_extra else {}),
             "step_factor": args.step_factor,
             "setup_s": setup_s,
         }
         if args.emulate_shard:
             out["emulated_shard_of"] = args.emulate_shard   # not a whole-job number: one rank's shard
         print(json.dumps(out), flush=True)
+    if dist is not None and args.sampler == "branch" and not args.no_network_check:
+        # after the line: one short network-joint trajectory through the library's
+        # communicator (RCCL over xGMI: the per-step all-reduce of the summed branch
+        # outputs, config C4's collective), reported on stderr.  A watchdog ends the
+        # process if the collective stalls, so the line above is never lost.
+        import threading
+        wd = threading.Timer(120.0, lambda: os._exit(0))
+        wd.daemon = True
+        wd.start()
+        library_comm()
+        dist.barrier()
+        t1 = time.perf_counter()
+        r = ctx.network_hmc_step(y_net, 20, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=0.1,
+                                 seed=31)
+        ctx.synchronize()
+        te = torch.tensor([time.perf_counter() - t1], device=dist_dev, dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            log(json.dumps({"network_check": {"n_gpus": world, "comm": "rccl" if backend == "nccl" else backend,
+                                              "L": 20, "status": r["status"], "steps_per_s": 20 / float(te.item()),
+                                              "trace_first_last": [r["trace"][0], r["trace"][-1]]}}))
+        wd.cancel()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -207,7 +207,7 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   auto forward_and_targets = [&](int k) -> int {
     int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
     if (r) return r;
-    launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->stream);
+    launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
     r = allreduce_device_f32(ctx, ctx->d_netsum, n);
     if (r) return r;
     launch_net_targets(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart, ctx->d_netrss + k,

@@ -175,7 +175,9 @@ void launch_update_joint(const DevState& st, const int32_t* branches, int32_t nb
 void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_q,
                                   uint64_t seed, hipStream_t s);
 #define BANN_JOINT_MAXQ 4608  // joint HMC: precisions per branch (ARD: m + hidden widths + L)
-void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, float* out, hipStream_t s);
+// scratch: residual_delta_scratch_floats(n)
+void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, float* out, float* scratch,
+                    hipStream_t s);
 // sum_e: in = sum over ranks of the branch outputs, out = the error e; part: net_scratch_doubles(n)
 void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
                         float bias, double* part, double* rss_out, hipStream_t s);

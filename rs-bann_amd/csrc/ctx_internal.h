@@ -145,7 +145,7 @@ struct bann_ctx {
   };
   std::vector<Rec> rec;  // indexed by branch
   // captured launch sequences of bann_hmc_step, keyed by plan shape, L and the by-value state
-  bool graph_replay = true;  // BANN_HMC_GRAPH=0: launch from the host every time
+  bool graph_replay = false;  // BANN_HMC_GRAPH=1: replay captured graphs (+5 % sequential; rocprofv3 crashes on them)
   std::vector<std::pair<std::string, hipGraphExec_t>> graphs;
   // leapfrog session
   Plan lf;

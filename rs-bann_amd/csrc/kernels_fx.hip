@@ -768,12 +768,29 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 // issued once the forward has read it (the head's prediction store first, so
 // the counted wait at the top never waits on a piece younger than the tile).
 // ===========================================================================
+#ifndef FWD_NS
+#define FWD_NS 4  // tile slots per wave: the stream runs FWD_NS tiles ahead (4: one workgroup per CU)
+#endif
+// all but the youngest k (0 .. 31) vector-memory operations of this wave are complete
+__device__ __forceinline__ void vm_wait_n(int k) {
+#define VMW(i) \
+  case i: asm volatile("s_waitcnt vmcnt(" #i ")" ::: "memory"); break;
+  switch (k) {
+    VMW(1) VMW(2) VMW(3) VMW(4) VMW(5) VMW(6) VMW(7) VMW(8) VMW(9) VMW(10) VMW(11) VMW(12) VMW(13) VMW(14)
+    VMW(15) VMW(16) VMW(17) VMW(18) VMW(19) VMW(20) VMW(21) VMW(22) VMW(23) VMW(24) VMW(25) VMW(26) VMW(27)
+    VMW(28) VMW(29) VMW(30) VMW(31)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+#undef VMW
+}
+
 template <int NL, int ACT, int NCH>
-__global__ void __launch_bounds__(64 * FX_WAVES, 2)
+__global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
     k_forward_fx(DevState st, const GradItem* __restrict__ items) {
   constexpr int NH = NL - 1;
   constexpr int NW = FX_WAVES;
-  __shared__ __attribute__((aligned(16))) char s_x[NW][2][FX_SLOT];
+  constexpr int NS = FWD_NS;
+  __shared__ __attribute__((aligned(16))) char s_x[NW][NS][FX_SLOT];
   __shared__ __attribute__((aligned(16))) char s_w0[8 * 1024];
   __shared__ __attribute__((aligned(16))) float s_hw[NL][20];
 
@@ -832,15 +849,16 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
 
+  // ring of NS slots: tile i of this wave in slot i % NS; the prologue fills the
+  // ring, each iteration refills the slot it consumed with the tile NS ahead
   int tt = tb + wave, sl = 0;
-  if (tt < te) {
-    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
-    if (tt + NW < te)
-      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
-  }
-  for (; tt < te; tt += NW, sl ^= 1) {
-    const bool more = tt + NW < te, more2 = tt + 2 * NW < te;
-    vm_wait(more ? nch : 0);  // this tile has landed; the next tile's nch pieces may fly
+  for (int j = 0; j < NS; ++j)
+    if (tt + j * NW < te)
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + j * NW, j, c);
+  for (; tt < te; tt += NW, sl = (sl + 1) % NS) {
+    int ahead = 0;  // later tiles of the ring in flight: their pieces are younger than this tile's
+    for (int j = 1; j < NS; ++j) ahead += tt + j * NW < te;
+    vm_wait_n(ahead * nch);
     const char* xs = &s_x[wave][sl][0];
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
     {
@@ -908,8 +926,8 @@ __global__ void __launch_bounds__(64 * FX_WAVES, 2)
     if (row < n) predb[row] = out;
     // every read of this slot has returned (the MFMAs consumed them): refill it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (more2)
-      for (int c = 0; c < nch; ++c) issue_chunk(tt + 2 * NW, sl, c);
+    if (tt + NS * NW < te)
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NS * NW, sl, c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

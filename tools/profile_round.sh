@@ -20,4 +20,4 @@ if [ -n "$PMC_MFMA" ]; then  # MFMA utilisation pass (SQ: 6 of 8 slots, GRBM: 2 
   timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_I8 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace --output-format csv -d $OUT/mfma -o bench -- \
     python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 --profile-iters 2 "$@" > $OUT/bench_mfma.json 2> $OUT/mfma.err || { echo "mfma pass failed"; exit 1; }
 fi
-cd $R && python3 tools/summarize_profile.py $TAG $OUT
+cd $R && python3 tools/summarize_profile.py $TAG $OUT "$@"

@@ -21,6 +21,16 @@ shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
 trace = list(csv.DictReader(open(find("trace", "*kernel_trace.csv"))))
 bench = json.loads(open(os.path.join(out, "bench_trace.json")).read().strip().splitlines()[-1])
 
+# the timed trajectory: bench.py runs the warmup trajectory, then the back-to-back
+# measurement session (a 2-step leapfrog session), then the timed trajectory;
+# each starts with one k_step_sizes launch (traj_prepare)
+trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+starts = [i for i, r in enumerate(trace) if "k_step_sizes" in r["Kernel_Name"]]
+timed = trace[starts[2]:starts[3] if len(starts) > 3 else len(trace)] if len(starts) > 2 else []
+tgrad = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_fused_grad" in r["Kernel_Name"]]
+tupd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_update" in r["Kernel_Name"]]
+tspan = ((int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])) / 1e6) if timed else 0.0
+
 # launches of the gradient kernel over the full branch set (grid = items x 576 threads)
 grad = [r for r in trace if "k_fused_grad" in r["Kernel_Name"]]
 big = max(int(r["Grid_Size_X"]) for r in grad)
@@ -52,6 +62,7 @@ fetch = pmc_bytes("fetch", "FETCH_SIZE") * 2.0   # gfx950: FETCH_SIZE counts 1/2
 write = pmc_bytes("write", "WRITE_SIZE", min)
 write_pred = pmc_bytes("write", "WRITE_SIZE", max)
 pmc = {"kernel": full[0]["Kernel_Name"], "config": bench["config"]["workload"],
+       "timed_trajectory_grad_ms_mean": statistics.mean(tgrad) if tgrad else None,
        "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
        "traffic_bytes_per_launch": fetch + write, "write_bytes_trajectory_end_launch": write_pred,
        "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
@@ -82,7 +93,8 @@ if mf:  # MFMA utilisation pass: per-counter medians over the full-branch-set gr
 json.dump(pmc, open(os.path.join(prof, f"{tag}_pmc.json"), "w"), indent=1)
 
 with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
-    f.write(f"# Profile {tag}: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline`\n\n")
+    f.write(f"# Profile {tag}: `rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline "
+            f"{' '.join(sys.argv[3:])}`\n\n")
     f.write(f"workload: {bench['config']['workload']}\n\n")
     f.write(f"bench line under the profiler: value {bench['value']:.2f} {bench['unit']}, "
             f"ms_per_step {bench['ms_per_step']:.3f}\n\n")
@@ -91,7 +103,17 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
             f"{statistics.median(dur):.3f} | {min(dur):.3f} |\n")
     f.write(f"| k_update (full set) | {len(upd)} | {statistics.mean(upd):.3f} | {statistics.median(upd):.3f} | "
             f"{min(upd):.3f} |\n\n")
-    f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.3f} ms\n\n")
+    if tgrad:
+        f.write(f"**Timed trajectory** ({len(tgrad)} gradient launches, {len(tupd)} update launches, "
+                f"span {tspan:.3f} ms for {bench['steps']} steps = {tspan / bench['steps']:.4f} ms per step): "
+                f"gradient launch mean {statistics.mean(tgrad):.4f} ms (median {statistics.median(tgrad):.4f}), "
+                f"update mean {statistics.mean(tupd):.4f} ms; "
+                f"algorithmic bytes / mean gradient launch = "
+                f"{pmc['alg_bytes_per_launch'] / (statistics.mean(tgrad) * 1e-3) / 1e9:.0f} GB/s = "
+                f"{pmc['alg_bytes_per_launch'] / (statistics.mean(tgrad) * 1e-3) / 8e12:.3f} of 8 TB/s\n\n")
+    f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.4f} ms "
+            f"({bench['roofline'].get('kernel_ms_source', '')}); back-to-back "
+            f"{bench['roofline'].get('kernel_ms_back_to_back', float('nan')):.4f} ms\n\n")
     f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB "
             f"({write_pred/1e9:.4f} GB at a trajectory's first/last launch, predictions included); "
             f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
