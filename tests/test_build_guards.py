@@ -36,3 +36,14 @@ def test_counted_fxl_instantiations_do_not_spill(tmp_path):
     assert all(spills[k] == 0 for k in counted), {k: spills[k] for k in counted}
     fx = [k for k in spills if k.startswith("_Z15k_fused_grad_fx")]
     assert fx and all(spills[k] == 0 for k in fx), {k: spills[k] for k in fx}
+    fwd = [k for k in spills if k.startswith("_Z12k_forward_fx")]
+    assert fwd and all(spills[k] == 0 for k in fwd), {k: spills[k] for k in fwd}
+
+
+def test_production_kernels_carry_no_profiling_switches():
+    """the ablation / stamp switches live in the profiling copy
+    (tools/profiling/kernels_fx_ablate.hip), not in the shipped kernels"""
+    for f in os.listdir(os.path.dirname(SRC)):
+        if f.endswith((".hip", ".h", ".cpp")):
+            txt = open(os.path.join(os.path.dirname(SRC), f)).read()
+            assert "#if BANN_ABLATE" not in txt and "FX_STAMP" not in txt, f

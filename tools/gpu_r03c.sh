@@ -19,5 +19,5 @@ for f in 0.12 0.15; do
 done
 timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --sampler sequential > $OUT/seq.json 2> $OUT/seq.err || { tail $OUT/seq.err; exit 1; }
 j $OUT/seq.json
-BANN_HMC_GRAPH=0 timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --sampler sequential > $OUT/seq_nog.json 2> $OUT/seq_nog.err || { tail $OUT/seq_nog.err; exit 1; }
+BANN_HMC_GRAPH=1 timeout -k 10 300 python bench.py --steps 20 --warmup 2 --no-cpu-baseline --sampler sequential > $OUT/seq_nog.json 2> $OUT/seq_nog.err || { tail $OUT/seq_nog.err; exit 1; }
 j $OUT/seq_nog.json

@@ -47,12 +47,24 @@
 #define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
 #define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
 #define FX_DROW 256       // delta0 digit image: 16 rows x 16 B per K group (read twice per tile)
-// The stream runs TWO tiles ahead in the same two slots: chunk c of tile t + 2
-// is issued into tile t's slot as soon as tile t's backward has read chunk c's
-// last window (the target piece once the head has read the target), so a piece
-// has a whole tile more to land than when it is issued in the forward (the
-// one-tile-ahead and burst variants are profiling builds:
-// tools/profiling/kernels_fx_ablate.hip)
+// FX_DEEP: the stream runs TWO tiles ahead in the same two slots -- chunk c of
+// tile t + 2 is issued into tile t's slot as soon as tile t's backward has read
+// chunk c's last window (the target piece once the head has read the target),
+// so a piece has a whole tile more to land than when it is issued in the forward
+// (profiling build ABL=524288: the one-tile-ahead stream, issued in the forward;
+// ABL=1048576: the deep stream's pieces issued after the backward in one burst)
+#if BANN_ABLATE & 1048576
+#define FX_SPREAD 0
+#else
+#define FX_SPREAD 1
+#endif
+#ifndef FX_DEEP
+#if BANN_ABLATE & 524288
+#define FX_DEEP 0
+#else
+#define FX_DEEP 1
+#endif
+#endif
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -124,6 +136,18 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 
 // NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
 // so the LDS reads of a whole phase issue back to back); 0 = any count <= 8.
+#if BANN_ABLATE & 16
+#define FX_STAMP(i)                                   \
+  do {                                                \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_last;                             \
+    t_last = t_;                                      \
+  } while (0)
+#else
+#define FX_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 template <int NL, int ACT, int NCH>
 __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
@@ -165,14 +189,17 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   }
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
   float zscale = st.fc[b].scale[g];
+#if !(BANN_ABLATE & 128)
   for (int c = wave; c < nch; c += NW)  // W0 digit image -> LDS (shared by the four waves)
     *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
         *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+#endif
   // retire the prologue loads and hide their provenance: inside the tile loop the
   // only vector-memory waits are the explicit, counted ones on this wave's DMAs
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+#if !(BANN_ABLATE & 262144)
   // head weights as wave-uniform values: scalar registers for the whole item (the
   // per-tile LDS broadcasts serialised the head on their latencies)
   float uW[NL][4][4], uB[NH][4];
@@ -187,6 +214,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 #pragma unroll
       for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l][16 + k]);
   }
+#endif
 
   // ---- per-lane LDS offsets ----
   const int gsw = g & 1;
@@ -208,13 +236,36 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   // (one 1 KiB piece per chunk, the target piece in the head): issued in one
   // burst the pieces back-pressure the wave for thousands of cycles.
   auto issue_chunk = [&](int tt, int sl, int c) {
+#if BANN_ABLATE & 8
+    return;  // profiling build: no genotype / target traffic
+#endif
+#if BANN_ABLATE & 131072
+    // profiling build: every DMA reads branch 0's first two tiles (L2-resident)
+    glds16(reinterpret_cast<const char*>(st.xu2) + lane * 16 + (int64_t)(tt & 1) * tile_bytes + c * 1024,
+           &s_x[wave][sl][c * 1024]);
+    return;
+#endif
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
+#if BANN_ABLATE & 2048
+  float ynx = 0.f;  // target of this lane's individual, one tile ahead (register, counted vmcnt)
+  auto issue_y = [&](int tt, int) {
+#if (BANN_ABLATE & 8) || (BANN_ABLATE & 64)
+    return;
+#endif
+    const int64_t row = 64 * (int64_t)tt + iota;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(ynx) : "v"(ybr + (row < n ? row : n - 1)) : "memory");
+  };
+#else
   auto issue_y = [&](int tt, int sl) {
+#if (BANN_ABLATE & 8) || (BANN_ABLATE & 64)
+    return;
+#endif
     const int64_t row = 64 * (int64_t)tt + iota;
     glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
   };
 
+#endif
   // ---- accumulators ----
   v4i acc[32];  // dW0 digit sums per 16-marker window u (lane: column g, marker 16u + i16)
 #pragma unroll
@@ -234,35 +285,67 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
   }
 
+#if BANN_ABLATE & 16
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime(), ntl = 0;
+#endif
   int tt = tb + wave, sl = 0;
+#if BANN_ABLATE & 16
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+#endif
   if (tt < te) {
     for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
-    if (tt + NW < te) {
+    if (FX_DEEP && tt + NW < te) {
       for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
       issue_y(tt + NW, 1);
     }
   }
   for (; tt < te; tt += NW, sl ^= 1) {
     const bool more = tt + NW < te;
-    const bool more2 = tt + 2 * NW < te;  // tile tt + 2 NW goes into this slot
+    const bool more2 = FX_DEEP && tt + 2 * NW < te;  // deep stream: tile tt + 2 NW goes into this slot
+    FX_STAMP(0);
     // tile tt (issued during tile tt - NW) has landed.  (An L2 prefetch of the
     // tile after it measured +3 %: with 8 waves/CU the L2 is already the DMA's
     // working set.)
-    // the nch + 1 pieces of tile tt + NW are younger (loads return in order; a
-    // younger pred store still outstanding only makes this wait longer)
-    vm_wait(more ? nch + 1 : 0);
+#if BANN_ABLATE & 2048
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(ynx)::"memory");
+#else
+    if (FX_DEEP) {
+      // the nch + 1 pieces of tile tt + NW are younger (loads return in order; a
+      // younger pred store still outstanding only makes this wait longer)
+      vm_wait(more ? nch + 1 : 0);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#endif
+    FX_STAMP(1);
     const char* xs = &s_x[wave][sl][0];
+#if BANN_ABLATE & 32
+    if (more) {
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, sl ^ 1, c);
+      issue_y(tt + NW, sl ^ 1);
+    }
+    acc[0][0] += xs[lane];
+    continue;
+#endif
 
     // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
     // (software pipelined: the LDS reads of chunk c + 1 fly while chunk c's
     // four MFMAs issue; sched barriers keep the compiler from hoisting more)
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
     // the forward at raised priority too (with the stream issued in the backward:
-    // -1.2 % per launch, A/B on one box)
+    // -1.2 % per launch, A/B tools/gpu_ab.sh; profiling build ABL=4096: priority 0)
+#if BANN_ABLATE & 4194304
+    __builtin_amdgcn_s_setprio(2);  // profiling build: the forward above the head
+#elif !(BANN_ABLATE & 4096)
     __builtin_amdgcn_s_setprio(1);
+#endif
     {
+#if BANN_ABLATE & 65536
+      constexpr int FD = 1;  // LDS reads one chunk ahead of their MFMAs
+#else
       constexpr int FD = 2;  // two chunks ahead: an LDS read's latency exceeds one chunk's 4 MFMAs
+#endif
       v4u Xq[FD];
       v4i Aq[FD];
 #pragma unroll
@@ -283,16 +366,24 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
           Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
         }
+        if (!FX_DEEP && more) issue_chunk(tt + NW, sl ^ 1, c);
         // fragment q = field q of every byte, kept in place (x 4^q, folded into the
         // digit combine below) except q = 3 (bits 6-7 would overflow int8)
         const v4i B0 = (v4i)(Xc & 0x03030303u);
         const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
         const v4i B2 = (v4i)(Xc & 0x30303030u);
         const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
+#if BANN_ABLATE & 4
+        facc[0] += B0 ^ Ac;
+        facc[1] += B1 ^ Ac;
+        facc[2] += B2 ^ Ac;
+        facc[3] += B3 ^ Ac;
+#else
         facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B0, facc[0], 0, 0, 0);
         facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B1, facc[1], 0, 0, 0);
         facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B2, facc[2], 0, 0, 0);
         facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
+#endif
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -300,7 +391,12 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // the head + digit phase is a dependent VALU chain: at raised priority it
     // takes the SIMD's issue slots ahead of the partner wave's independent
     // MFMA/unpack stream (measured -1 %)
+#if BANN_ABLATE & 2097152
+    __builtin_amdgcn_s_setprio(2);  // profiling build: the head above the forward
+#else
     __builtin_amdgcn_s_setprio(1);
+#endif
+    FX_STAMP(2);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
@@ -313,11 +409,44 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // ---- head: one individual per lane ----
     const int64_t row = 64 * (int64_t)tt + iota;
     const bool valid = row < n;
+#if BANN_ABLATE & 2048
+    const float yv = ynx;
+#else
     const float yv = s_y[wave][sl][lane];
+#endif
+    if (!FX_DEEP && more) issue_y(tt + NW, sl ^ 1);
     float d[4];
+#if BANN_ABLATE & 1
+    d[0] = z0 * 1e-3f - yv;
+    d[1] = z1 * 1e-3f;
+    d[2] = z2 * 1e-3f;
+    d[3] = z3 * 1e-3f;
+    (void)valid;
+    if (false)
+#endif
     {
+#if BANN_ABLATE & 262144
+      float Wh[NL][4][4], Bh[NH][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l][4 * j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Wh[l][j][k] = r4[k];
+          }
+        }
+        if (l < NH) {
+          const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l][16]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
+        }
+      }
+#else
       const auto& Wh = uW;
       const auto& Bh = uB;
+#endif
       float z[NH][4], a[NH][4];
       z[0][0] = z0 + Bh[0][0];
       z[0][1] = z1 + Bh[0][1];
@@ -379,6 +508,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       issue_y(tt + 2 * NW, sl);
     }
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(3);
     // the backward's first genotype windows: their LDS reads fly under the digit phase
     constexpr int PD = 8;
     uint32_t wq[PD];
@@ -421,44 +551,107 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         if (NCH != 0 || u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
     }
     v4u w;
+#if BANN_ABLATE & 8192
+    constexpr int kslot_sh = 0;
+#else
     // this lane's individual sits in K-group p = g of the backward operand, whose
     // genotype codes stay in place (x 4^p, p = 1, 2): pre-divide its digits by 4^p
     const int kslot_sh = g == 1 ? 2 : g == 2 ? 4 : 0;
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - kslot_sh - (R[k] ? R[k] : 255));
     *reinterpret_cast<v4u*>(sd_w) = w;
 
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
+    FX_STAMP(4);
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
       // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
       auto unpack = [](uint32_t wv) -> v4i {
+#if BANN_ABLATE & 8192
+        return v4i{(int)(wv & 0x03030303u), (int)((wv >> 2) & 0x03030303u), (int)((wv >> 4) & 0x03030303u),
+                   (int)((wv >> 6) & 0x03030303u)};
+#else
         return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
                    (int)((wv >> 6) & 0x03030303u)};
+#endif
       };
+#if !(BANN_ABLATE & 32768)
       // window u + 2 is unpacked beside window u's MFMA: the MFMA's B operand was
       // written two iterations earlier, so no VALU -> MFMA hazard padding per window
       v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);
+#endif
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
         if (NCH == 0 && u >= 4 * nch) continue;
+#if BANN_ABLATE & 32768
+        const uint32_t wv = wq[u % PD];
+        if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+        const v4i Bv = unpack(wv);
+#else
         const v4i Bv = Bn;
         Bn = Bn2;
         if (u + 2 < 32 && (NCH != 0 || u + 2 < 4 * nch)) Bn2 = unpack(wq[(u + 2) % PD]);
-        if (more2 && (u & 3) == 1) {  // window 4c + 3, chunk c's last, is unpacked: refill chunk c
+        if (FX_SPREAD && more2 && (u & 3) == 1) {  // window 4c + 3, chunk c's last, is unpacked: refill chunk c
           asm volatile("" ::"v"(Bn2[0]), "v"(Bn2[1]), "v"(Bn2[2]), "v"(Bn2[3]));
           issue_chunk(tt + 2 * NW, sl, u >> 2);
         }
         if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))  // slot of window u, consumed two iterations ago
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+#endif
+#if BANN_ABLATE & 2
+        acc[u] += Bv ^ A;
+#else
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
+#endif
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+#if BANN_ABLATE & 1048576
+    // profiling build: tile tt + 2 NW's pieces issued after the backward, in one burst
+    if (more2) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + 2 * NW, sl, c);
+    }
+#endif
+    FX_STAMP(5);
+#if BANN_ABLATE & 16
+    ++ntl;
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if BANN_ABLATE & 256
+  {  // keep every accumulator live (no dead-code elimination of the tile loop)
+    int x = 0;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) x ^= acc[u][0] ^ acc[u][1] ^ acc[u][2] ^ acc[u][3];
+    float f = (float)rss;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f += dWo[k];
+#pragma unroll
+      for (int l = 0; l < NH; ++l) f += db[l][k];
+#pragma unroll
+      for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) f += dW[l][j][k];
+    }
+    if (x == 0x7fffffff || f == 1234.5f) st.part[0] = 1.f;
+    return;
+  }
+#endif
+#if BANN_ABLATE & 16
+  // p6 / p7: the loop's 100 MHz real time and shader cycles (their ratio: the clock)
+  ph[6] = __builtin_amdgcn_s_memrealtime() - rt0;
+  ph[7] = __builtin_amdgcn_s_memtime() - mt0;
+  if (lane == 0 && st.dbg) {
+    for (int i = 0; i < 8; ++i) atomicAdd(&st.dbg[i], ph[i]);
+    atomicAdd(&st.dbg[15], ntl);
+  }
+#endif
 
   // ---- workgroup reduction (fixed order: deterministic) ----
   {
@@ -792,6 +985,9 @@ void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems
 #ifndef FXL_DPRE
 #define FXL_DPRE 31  // backward window after which the next tile's first digit loads issue (earlier: spills)
 #endif
+#ifndef FXL_ABL
+#define FXL_ABL 0  // profiling-only ablations (1: no W0 digit loads, 2: no per-tile barrier); 0 in shipped builds
+#endif
 
 // one global_load_dwordx4 outside the compiler's wait model (counted by hand)
 __device__ __forceinline__ v4i ld_counted(const char* p) {
@@ -864,6 +1060,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+#if !(BANN_ABLATE & 262144)
   float uW[NL][4][4], uB[NH][4];  // head weights in scalar registers (as fx)
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
@@ -876,6 +1073,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 #pragma unroll
       for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l * 20 + 16 + k]);
   }
+#endif
 
   const int gsw = g & 1;
   const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
@@ -927,6 +1125,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     issue_y(tt, 0);
   }
   auto ldig = [&](int off) -> v4i {
+#if FXL_ABL & 1
+    return v4i{off, 1, 2, 3};  // profiling build: no digit loads
+#endif
     if constexpr (CNT) return ld_counted(dsrc + off);
     return *reinterpret_cast<const v4i*>(dsrc + off);
   };
@@ -940,6 +1141,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 
     // ---- forward: partial Z0 over this wave's block ----
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+#if BANN_ABLATE & 8388608
+    __builtin_amdgcn_s_setprio(1);  // profiling build: the forward at raised priority (as fx)
+#endif
     {
       v4i Dg[8];
       Dg[0] = Dn0;
@@ -951,7 +1155,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
         v4u Xn = Xc;
         if (c + 1 < 8 && (FULL || c + 1 < cw))
           Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
-        if constexpr (CNT) {
+        if constexpr (CNT && !(FXL_ABL & 1)) {
           // loads younger than digit load c (issue order below: D(c+2) then
           // piece c per chunk, the pieces issued on every tile so the count is a
           // compile-time constant -- a runtime count would need a branch, and the
@@ -987,7 +1191,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     // ---- Z0 exchange: every wave sums the NW partials in wave order ----
     v4f* xw = s_xch + (xb * NW) * 64;
     lds_st_v4f(xw + wave * 64 + lane, v4f{z0, z1, z2, z3});
+#if !(FXL_ABL & 2)
     LDS_BARRIER();
+#endif
     {
       v4f zs = xw[lane];
       for (int w = 1; w < NW; ++w) zs += xw[w * 64 + lane];
@@ -1004,8 +1210,28 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     if (more) issue_y(tt + 1, sl ^ 1);
     float d[4];
     {
+#if BANN_ABLATE & 262144
+      float Wh[NL][4][4], Bh[NH][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        if (l >= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l * 20 + 4 * j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) Wh[l][j][k] = r4[k];
+          }
+        }
+        if (l < NH) {
+          const v4f r4 = *reinterpret_cast<const v4f*>(&s_hw[l * 20 + 16]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) Bh[l][k] = r4[k];
+        }
+      }
+#else
       const auto& Wh = uW;
       const auto& Bh = uB;
+#endif
       float z[NH][4], a[NH][4];
       z[0][0] = z0 + Bh[0][0];
       z[0][1] = z1 + Bh[0][1];
@@ -1114,15 +1340,24 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
         return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
                    (int)((wv >> 6) & 0x03030303u)};
       };
+#if !(BANN_ABLATE & 32768)
       v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);  // two windows ahead of their MFMA (as in fx)
+#endif
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
         if (!FULL && u >= 4 * cw) continue;
+#if BANN_ABLATE & 32768
+        const uint32_t wv = wq[u % PD];
+        if (u + PD < 32 && (FULL || u + PD < 4 * cw))
+          wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+        const v4i Bv = unpack(wv);
+#else
         const v4i Bv = Bn;
         Bn = Bn2;
         if (u + 2 < 32 && (FULL || u + 2 < 4 * cw)) Bn2 = unpack(wq[(u + 2) % PD]);
         if (u + PD < 32 && (FULL || u + PD < 4 * cw))
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+#endif
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         // the next tile's first two digit operands, half a backward ahead of their use
