@@ -208,7 +208,7 @@ def main():
     if args.step_factor is None:
         # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
         # curvature, c = 1 rejects every trajectory; c = 0.1 accepts ~0.9 at L = 100 (tools/gpu_c5sweep.sh)
-        args.step_factor = {"c5": 0.1, "c3def": 0.02}.get(args.config, 1.0)
+        args.step_factor = {"c5": 0.02 if args.hidden_bf16 else 0.1, "c3def": 0.02}.get(args.config, 1.0)
         if args.sampler == "network":   # the joint state's energy error sums over all 1000 branches
             args.step_factor = {"c3": 0.12}.get(args.config, 0.1 * args.step_factor)
     heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
