@@ -838,6 +838,12 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
       o += 2 * ntile * r4(d.widths[h.L - 2]);
       d.gx_rss = (int32_t)o;
       o += r4(2 * ntile);
+      d.gx_op = (int32_t)o;
+      o += 2 * ((d.widths[h.L - 2] + 63) / 64) * gx_rows;
+      d.gx_e = (int32_t)o;
+      o += gx_rows;
+      d.gx_wps = (int32_t)o;
+      if (h.L >= 3) o += r4((3ll * d.widths[h.L - 2] * ((d.win[h.L - 2] + 31) & ~31) + 1) / 2);
       for (int l = 0; l < h.L - 1; ++l) {
         d.gx_ld[l] = (int32_t)r4(d.widths[l]);
         d.gx_a[l] = (int32_t)o;

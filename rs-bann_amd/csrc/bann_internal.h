@@ -48,6 +48,9 @@ struct BranchDev {
   int32_t gx_ld[BANN_MAXL];   //   row stride: w_l rounded up to 4
   int32_t gx_dwo;             // head: f64 dW_out partials [tile][S]
   int32_t gx_rss;             // head: f64 rss partials [tile]
+  int32_t gx_op;              // FWD of the summary layer: f32 partial outputs A_s w_out [2 ceil(S/64)][rows]
+  int32_t gx_e;               // head: the output error e = out - y [rows] (0 past n)
+  int32_t gx_wps;             // Wp_s (s = L-2 >= 1) with row k scaled by w_out[k], as three bf16 planes like gx_wp (lazy head BWD_s)
   int32_t gx_w0p;             // W0 / sigma as three bf16 planes [3][w0][64 nchunks] (masked layer on bf16 MFMA)
   int32_t gx_wp[BANN_MAXL];   // Wp_l, 1 <= l < L-1, as three bf16 planes [3][w_l][win_l rounded up to 32] (hidden GEMMs)
   // precision coordinates (precision_vec order, params.rs:272-289) for joint HMC

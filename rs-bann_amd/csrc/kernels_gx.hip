@@ -182,10 +182,33 @@ __device__ __forceinline__ void geno_store_mi(uint32_t g, float* L) {
 
 }  // namespace
 
+// a lane of the same row of 16 (DPP control CTRL)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 // h'(z) as a function of a = h(z) for the activations where it is one (tanh:
 // 1 - a^2; ReLU / leaky ReLU: a > 0 <=> z > 0; identity): those layers store A_l
 // only, and the backward phases form H_l from it (SiLU keeps H_l)
 __device__ __forceinline__ bool dh_from_a(int act) { return act != 3; }
+// the same without branches: h' = base(a) - tq a^2 with base = bp (a > 0), bn (a < 0),
+// bz (a = 0) and the four constants of the activation (identical values)
+struct DhA {
+  float tq, bp, bn, bz;
+};
+__device__ __forceinline__ DhA dh_a_consts(int act) {
+  switch (act) {
+    case 0: return DhA{1.f, 1.f, 1.f, 1.f};
+    case 1: return DhA{0.f, 1.f, 0.f, 0.f};
+    case 2: return DhA{0.f, 1.f, 0.01f, 0.f};
+    default: return DhA{0.f, 1.f, 1.f, 1.f};
+  }
+}
+__device__ __forceinline__ float dh_a(float a, const DhA& k) {
+  const float base = a > 0.f ? k.bp : (a < 0.f ? k.bn : k.bz);
+  return k.tq != 0.f ? 1.f - a * a : base;
+}
 __device__ __forceinline__ float act_dh_a(float a, int act) {
   switch (act) {
     case 0: return 1.f - a * a;
@@ -204,7 +227,8 @@ __device__ __forceinline__ float act_dh_a(float a, int act) {
 template <int PH, bool F64>
 __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev& bd, float* S, int l, int tm, int tn,
                                             int split, int wi, int wo, int ar, int bc, int li, int lq, const v4f (&acc)[4],
-                                            const double (&dacc)[4][4], double cs, const double* cs_col) {
+                                            const double (&dacc)[4][4], double cs, const double* cs_col,
+                                            bool lazy = false, double cs2 = 0.0, const float* pre = nullptr) {
   const int t = threadIdx.x;
   if constexpr (PH == GX_FWD0 || PH == GX_FWD) {
     const int lay = PH == GX_FWD0 ? 0 : l;
@@ -212,6 +236,19 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     float* Ao = S + bd.gx_a[lay];
     float* Ho = S + bd.gx_h[lay];
     const int64_t ld = bd.gx_ld[lay];
+    // the summary layer (lazy head, k_gx_head): the wave's partial of out = A_s w_out
+    // over its 32 columns, per row
+    const bool head = PH == GX_FWD && l == bd.L - 2 && dh_from_a(bd.act);
+    const float* wout = S + bd.gx_w[bd.L - 1];
+    float po[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // the lane's two columns' bias and w_out (pre: loaded by the caller before its K loop)
+    float bq[2], wq[2];
+#pragma unroll
+    for (int Y = 0; Y < 2; ++Y) {
+      const int j = 64 * tn + bc + 16 * Y + li;
+      bq[Y] = pre ? pre[Y] : (j < wo ? bias[j] : 0.f);
+      wq[Y] = pre ? pre[2 + Y] : (head && j < wo ? wout[j] : 0.f);
+    }
     // the activation as a compile-time kind (activations.h)
     auto out = [&](auto kind) {
       constexpr int ACT = decltype(kind)::value;
@@ -219,7 +256,8 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
       for (int x = 0; x < 4; ++x) {
         const int j = 64 * tn + bc + 16 * (x & 1) + li;
         if (j >= wo) continue;
-        const float bj = bias[j];
+        const float bj = bq[x & 1];
+        const float wj = wq[x & 1];
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
           const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
@@ -227,6 +265,7 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
           const float a = ACT == 0 ? fast_tanh(z) : act_h_t<ACT>(z);  // tanh to ~2 ulp (layer outputs feed GEMMs)
           Ao[row * ld + j] = a;
           if constexpr (ACT == 3) Ho[row * ld + j] = act_dh_t<ACT>(z, a);
+          po[x >> 1][y] += a * wj;  // columns 16 (x & 1) + li: Y = 0 then 1
         }
       }
     };
@@ -236,6 +275,21 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
       case 2: out(std::integral_constant<int, 2>{}); break;
       case 3: out(std::integral_constant<int, 3>{}); break;
       default: out(std::integral_constant<int, 4>{}); break;
+    }
+    if (head) {  // fixed butterfly over the 16 column lanes; lane li = 0 writes slot 2 tn + (bc / 32)
+      const int64_t rows = gx_rows(st);
+      float* op = S + bd.gx_op + (int64_t)(2 * tn + (bc >> 5)) * rows;
+#pragma unroll
+      for (int X = 0; X < 2; ++X)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          float v = po[X][y];
+          v += dpp_f<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+          v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+          v += dpp_f<0x141>(v);  // row_half_mirror
+          v += dpp_f<0x140>(v);  // row_mirror: every lane of the 16 holds the same sum
+          if (li == 0) op[64 * (int64_t)tm + ar + 16 * X + 4 * lq + y] = v;
+        }
     }
   } else if constexpr (PH == GX_BWD) {
     float* Hd = S + bd.gx_h[l - 1];
@@ -251,7 +305,8 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
       for (int y = 0; y < 4; ++y) {
         const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
         const float h = fa ? act_dh_a(Ad[row * ld + j], act) : Hd[row * ld + j];
-        Hd[row * ld + j] = h * acc[x][y];  // delta = h'(z) * (delta_next W^T)
+        // delta = h'(z) * (delta_next W^T); lazy head: the accumulator lacks e of the row
+        Hd[row * ld + j] = h * (lazy ? pre[4 * (x >> 1) + y] * acc[x][y] : acc[x][y]);
       }
     }
   } else {
@@ -267,6 +322,7 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
         const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
         if (i >= wi) continue;
         double v = dacc[x][y];
+        if (PH == GX_GRAD && lazy) v *= (double)pre[x & 1];  // lazy head: times w_out of the column
         if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
           const float sg = st.sigma[bd.mk_off + i];
           v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_col[bc + 16 * (x & 1) + li]) / (double)sg : 0.0;
@@ -274,7 +330,10 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
         part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
       }
     }
-    if (tm == 0 && t < GX_T && 64 * tn + t < wo) part[bd.boff[lay] + 64 * tn + t] = (float)cs;  // db_l
+    if (tm == 0 && t < GX_T && 64 * tn + t < wo) {
+      part[bd.boff[lay] + 64 * tn + t] = (float)cs;                // db_l
+      if (lazy) part[bd.woff[bd.L - 1] + 64 * tn + t] = (float)cs2;  // dW_out = A_s^T e (lazy head)
+    }
   }
 }
 
@@ -833,6 +892,12 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int li = lane & 15, lq = lane >> 4;
   const int ar = 32 * (wv >> 1), bc = 32 * (wv & 1);
+  // lazy head (k_gx_head): delta_s = h'(A_s) * (e w_out) is formed while staging
+  // from A_s, the error e and w_out instead of being stored; GRAD_s's column sums
+  // also give dW_out = A_s^T e
+  const bool lazy = PH != GX_FWD && l == bd.L - 2 && dh_from_a(bd.act);
+  const float* ev = S + bd.gx_e;
+  const float* wout = S + bd.gx_w[bd.L - 1];
 
   int64_t kb0 = 0, kb1, kcount;
   const float* Am;
@@ -848,7 +913,7 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     wo = bd.widths[l];
   } else if constexpr (PH == GX_BWD) {  // delta_l Wp_l: A = delta_l [individual][out], B = Wp_l [out = k][in]
     kcount = bd.widths[l];
-    Am = S + bd.gx_h[l];
+    Am = S + (lazy ? bd.gx_a[l] : bd.gx_h[l]);
     lda = bd.gx_ld[l];
     Bm = S + bd.gx_w[l];
     ldb = bd.gx_wld[l];
@@ -859,7 +924,7 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     Am = S + bd.gx_a[l - 1];
     lda = bd.gx_ld[l - 1];
     wi = bd.widths[l - 1];
-    Bm = S + bd.gx_h[l];
+    Bm = S + (lazy ? bd.gx_a[l] : bd.gx_h[l]);
     ldb = bd.gx_ld[l];
     wo = bd.widths[l];
     kb0 = 2 * ((int64_t)ntile * split / ns);  // 64-row tiles -> 32-deep K blocks
@@ -881,7 +946,8 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
   // the in width are zero (the planes' padding covers the rest of a piece)
   constexpr bool BP = PH != GX_GRAD;
   v4i rbp[3];
-  const __bf16* Wp3 = BP ? reinterpret_cast<const __bf16*>(S + bd.gx_wp[l]) : nullptr;
+  const __bf16* Wp3 = BP ? reinterpret_cast<const __bf16*>(S + (PH == GX_BWD && lazy ? bd.gx_wps : bd.gx_wp[l]))
+                         : nullptr;
   const int64_t l3 = BP ? ((bd.win[l] + 31) & ~31) : 0, p3 = BP ? (int64_t)bd.widths[l] * l3 : 0;
   auto load_bp = [&](v4i (&rp_)[3], int64_t kb) {
     int64_t row, col;
@@ -914,7 +980,74 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
 #pragma unroll
     for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
   }
+  // lazy head: delta_s = h'(A_s) * e * w_out is never stored.  BWD_s: A = h'(A_s),
+  // B = the w_out-scaled planes of Wp_s (k_gx_prep), the epilogue multiplies row i
+  // by e_i; GRAD_s: B = h'(A_s) * e (e of the block's rows, per K block), the
+  // epilogue multiplies column j by w_out_j; its column sums give db_s (times w_out)
+  // and dW_out = A_s^T e (f64, from the raw A_s values)
+  float le[2] = {0.f, 0.f};
+  double csq[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD_s, tm == 0: dW_out column sums
+  auto lazy_load = [&](int64_t kb) {
+    if constexpr (PH == GX_GRAD) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) le[u] = ev[GX_KB * kb + ((t + 256 * u) >> 4)];
+    }
+  };
+  const DhA dk = dh_a_consts(bd.act);
+  const bool tanh_act = bd.act == 0;
+  auto lazy_h = [&](Blk2& r) {  // r = h'(A_s) (* e of the row: GRAD)
+    if (tanh_act) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float a = r.v[u][c];
+          r.v[u][c] = PH == GX_GRAD ? (1.f - a * a) * le[u] : 1.f - a * a;
+        }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float h = dh_a(r.v[u][c], dk);
+          r.v[u][c] = PH == GX_GRAD ? h * le[u] : h;
+        }
+    }
+  };
+  auto lazy_dwo = [&](const Blk2& r) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) csq[c] += (double)r.v[u][c] * (double)le[u];
+  };
+  // values the epilogue needs, loaded before the K loop (gx_epilogue): FWD the bias
+  // and w_out of the lane's two columns, lazy BWD_s the e of its eight rows, lazy
+  // GRAD_s w_out of its two columns
+  float pre[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (PH == GX_FWD) {
+    const bool head = l == bd.L - 2 && dh_from_a(bd.act);
+#pragma unroll
+    for (int Y = 0; Y < 2; ++Y) {
+      const int j = 64 * tn + bc + 16 * Y + li;
+      pre[Y] = j < wo ? S[bd.gx_b[l] + j] : 0.f;
+      pre[2 + Y] = head && j < wo ? wout[j] : 0.f;
+    }
+  } else if constexpr (PH == GX_BWD) {
+    if (lazy)
+#pragma unroll
+      for (int X = 0; X < 2; ++X)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) pre[4 * X + y] = ev[64 * (int64_t)tm + ar + 16 * X + 4 * lq + y];
+  } else {
+    if (lazy)
+#pragma unroll
+      for (int Y = 0; Y < 2; ++Y) {
+        const int j = 64 * tn + bc + 16 * Y + li;
+        pre[Y] = j < wo ? wout[j] : 0.f;
+      }
+  }
   auto load = [&](int64_t kb) {
+    if (lazy) lazy_load(kb);
 #if !(GX_ABL & 2)
     blk2_load<ARK>(ra, Am, lda, bnd_a(kb));
 #endif
@@ -926,6 +1059,14 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
   auto stage = [&](int64_t kb, int buf) {
     __bf16* As = As_[buf];
     __bf16* Bs = Bs_[buf];
+    if constexpr (PH == GX_BWD) {
+      if (lazy) lazy_h(ra);
+    } else if constexpr (PH == GX_GRAD) {
+      if (lazy) {
+        if (want_cs) lazy_dwo(rb);
+        lazy_h(rb);
+      }
+    }
 #if !(GX_ABL & 2)  // profiling builds: GX_ABL 1 / 2 skip the B / A staging, 4 the MFMAs
     blk2_store<ARK, false>(ra, bnd_a(kb), As, csa);
 #endif
@@ -1011,15 +1152,25 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
       dacc[x][3] += (double)acc[x].w;
     }
   }
-  double cs = 0.0;
+  double cs = 0.0, cs2 = 0.0;
   if (want_cs) {  // 16 threads per 4-column group, added in thread order (deterministic)
 #pragma unroll
     for (int x = 0; x < 4; ++x) cs_s[t >> 4][4 * (t & 15) + x] = csp[x];
     __syncthreads();
     if (t < GX_T)
       for (int k = 0; k < 16; ++k) cs += cs_s[k][t];
+    if (lazy) {  // db_s = w_out * (column sums of h'(A_s) e); the dW_out column sums, same order
+      cs *= (t < GX_T && 64 * tn + t < wo) ? (double)wout[64 * tn + t] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int x = 0; x < 4; ++x) cs_s[t >> 4][4 * (t & 15) + x] = csq[x];
+      __syncthreads();
+      if (t < GX_T)
+        for (int k = 0; k < 16; ++k) cs2 += cs_s[k][t];
+    }
   }
-  gx_epilogue<PH, F64>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, nullptr);
+  gx_epilogue<PH, F64>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, nullptr, lazy, cs2,
+                       PH == GX_FWD || lazy ? pre : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1070,6 +1221,20 @@ __global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __r
       P3[2 * tot + e] = ll;
     }
   }
+  if (bd.L >= 3 && dh_from_a(bd.act)) {  // lazy head: w_out[k] Wp_s[k][j] as three planes (k_gx_gemm_x3 BWD_s)
+    const int l = bd.L - 2, l3 = (bd.win[l] + 31) & ~31;
+    const float* wo = th + bd.woff[bd.L - 1];
+    __bf16* P3 = reinterpret_cast<__bf16*>(S + bd.gx_wps);
+    const int64_t tot = (int64_t)bd.widths[l] * l3;
+    for (int64_t e = g0; e < tot; e += gs) {
+      const int k = (int)(e / l3);
+      __bf16 hh, mm, ll;
+      split3(wo[k] * wval(l, k, (int)(e % l3)), hh, mm, ll);
+      P3[e] = hh;
+      P3[tot + e] = mm;
+      P3[2 * tot + e] = ll;
+    }
+  }
   // c0 = b0 - sum_j mu_j Wp_0[k][j] (f64): one wave per unit, lane-strided partials
   // added in a fixed order; the other biases
   {
@@ -1093,7 +1258,15 @@ __global__ void __launch_bounds__(256) k_gx_prep(DevState st, const int32_t* __r
 // over the tile's 64 rows.  dW_out and the rss leave per-tile f64 partials in the
 // scratch; k_gx_head_red adds them per split in tile order (deterministic).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __restrict__ blist) {
+// Lazy head (fuse, the bf16-plane path, a summary layer after a hidden one and an
+// activation whose h' is a function of A): the summary layer's FWD epilogue left
+// the per-wave partials of out in gx_op, so the head only adds them (in slot order),
+// forms e, pred and the rss, and writes e; BWD_s and GRAD_s form delta_s while
+// staging and GRAD_s adds dW_out: A_s is not read here and delta_s never stored.
+__device__ __forceinline__ bool gx_lazy_head(const BranchDev& bd, int fuse) {
+  return fuse && bd.L >= 3 && dh_from_a(bd.act);
+}
+__global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __restrict__ blist, int fuse) {
   __shared__ float e_s[GX_T];
   __shared__ double r_s[4];
   const int b = blist[blockIdx.y];
@@ -1102,6 +1275,25 @@ __global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __r
   if (tile >= (st.nfrag + 3) / 4) return;
   float* S = gx_base(st, bd);
   const int sl = bd.L - 2, Sw = bd.widths[sl];
+  if (gx_lazy_head(bd, fuse)) {
+    const int t = threadIdx.x;
+    if (t >= GX_T) return;
+    const int64_t rows = gx_rows(st), row = 64 * (int64_t)tile + t;
+    const int ns = 2 * ((Sw + 63) / 64);
+    const float* op = S + bd.gx_op + row;
+    double acc = 0.0;
+    for (int k = 0; k < ns; ++k) acc += (double)op[k * rows];
+    const float out = (float)acc;
+    float e = 0.f;
+    if (row < st.n) {
+      e = out - st.y[bd.y_off + row];
+      st.pred[bd.y_off + row] = out;
+    }
+    S[bd.gx_e + row] = e;
+    const double rss = wave_sum_d((double)e * (double)e);
+    if (t == 0) ((double*)(S + bd.gx_rss))[tile] = rss;
+    return;
+  }
   const float* A = S + bd.gx_a[sl];
   float* H = S + bd.gx_h[sl];
   const int64_t ld = bd.gx_ld[sl];
@@ -1146,7 +1338,7 @@ __global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __r
 }
 
 // grid (splits, branches): dW_out and rss of each split, tiles in order
-__global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t* __restrict__ blist) {
+__global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t* __restrict__ blist, int fuse) {
   const int b = blist[blockIdx.y];
   const BranchDev& bd = st.br[b];
   const int split = blockIdx.x;
@@ -1157,7 +1349,7 @@ __global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t*
   const int Sw = bd.widths[bd.L - 2];
   const double* dwo = (const double*)(S + bd.gx_dwo);
   float* part = st.part + bd.part_off + (int64_t)split * bd.P + bd.woff[bd.L - 1];
-  for (int k = threadIdx.x; k < Sw; k += 256) {
+  for (int k = threadIdx.x; k < Sw && !gx_lazy_head(bd, fuse); k += 256) {  // lazy: GRAD_s writes dW_out
     double d = 0.0;
     for (int tl = t0; tl < t1; ++tl) d += dwo[(int64_t)tl * Sw + k];
     part[k] = (float)d;
@@ -1176,18 +1368,22 @@ __global__ void __launch_bounds__(256) k_gx_head_red(DevState st, const int32_t*
 void launch_gx_prep(const DevState& st, const int32_t* blist, int nb, hipStream_t s) {
   if (nb > 0) hipLaunchKernelGGL(k_gx_prep, dim3(nb, GX_PREP_Y), dim3(256), 0, s, st, blist);
 }
+static bool gx_exact() {
+  const char* ex = getenv("BANN_GX_EXACT");  // 1: every phase on the exact-f32 MFMA path
+  return ex && atoi(ex) != 0;
+}
 void launch_gx_head(const DevState& st, const int32_t* blist, int nb, int max_splits, hipStream_t s) {
   if (nb <= 0) return;
-  hipLaunchKernelGGL(k_gx_head, dim3((st.nfrag + 3) / 4, nb), dim3(256), 0, s, st, blist);
-  hipLaunchKernelGGL(k_gx_head_red, dim3(max_splits, nb), dim3(256), 0, s, st, blist);
+  const int fuse = gx_exact() ? 0 : 1;  // the lazy head pairs with the bf16-plane BWD / GRAD (k_gx_gemm_x3)
+  hipLaunchKernelGGL(k_gx_head, dim3((st.nfrag + 3) / 4, nb), dim3(256), 0, s, st, blist, fuse);
+  hipLaunchKernelGGL(k_gx_head_red, dim3(max_splits, nb), dim3(256), 0, s, st, blist, fuse);
 }
 void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, const int32_t* prefix, int nb,
                     int total, hipStream_t s) {
   if (nb <= 0 || total <= 0) return;
   const int per = (total + 7) / 8;
   const dim3 g(8 * per), blk(256);
-  const char* ex = getenv("BANN_GX_EXACT");  // 1: the masked layer on the exact-f32 MFMA path
-  const bool exact = ex && atoi(ex) != 0;
+  const bool exact = gx_exact();
   if (!exact && ph == GX_FWD0) {
     hipLaunchKernelGGL(k_gx_gemm_b3<GX_FWD0>, g, blk, 0, s, st, blist, prefix, nb, total, per);
     return;
