@@ -60,22 +60,24 @@ __device__ __forceinline__ int64_t gx_rows(const DevState& st) { return (int64_t
 __device__ __forceinline__ float* gx_base(const DevState& st, const BranchDev& bd) { return st.scr + bd.scr_off; }
 
 // the tile numbering of a phase for one branch (must match gx_tiles on the host)
+// (tile edges TM x TN: 64 x 64, the hidden FWD / BWD of k_gx_gemm_x3 128 x 128)
 __device__ __forceinline__ void gx_dims(const DevState& st, const BranchDev& bd, int ph, int l, int& tmc, int& tnc,
-                                        int& ns) {
+                                        int& ns, int TM = 64, int TN = 64) {
   const int ntile = (st.nfrag + 3) / 4;
+  const int rt = (ntile * 64 + TM - 1) / TM;
   ns = 1;
   if (ph == GX_FWD0) {
     tmc = ntile;
     tnc = (bd.widths[0] + 63) / 64;
   } else if (ph == GX_FWD) {
-    tmc = ntile;
-    tnc = (bd.widths[l] + 63) / 64;
+    tmc = rt;
+    tnc = (bd.widths[l] + TN - 1) / TN;
   } else if (ph == GX_BWD) {
-    tmc = ntile;
-    tnc = (bd.widths[l - 1] + 63) / 64;
+    tmc = rt;
+    tnc = (bd.widths[l - 1] + TN - 1) / TN;
   } else if (ph == GX_GRAD) {
-    tmc = (bd.widths[l - 1] + 63) / 64;
-    tnc = (bd.widths[l] + 63) / 64;
+    tmc = (bd.widths[l - 1] + TM - 1) / TM;
+    tnc = (bd.widths[l] + TN - 1) / TN;
     ns = bd.nsplits;
   } else {  // GX_GRAD0
     tmc = bd.nchunks;
@@ -218,18 +220,22 @@ __device__ __forceinline__ float act_dh_a(float a, int act) {
   }
 }
 
-// the epilogue of a 64 x 64 output tile: lane holds rows ar + 16 X + 4 lq + y and
-// columns bc + 16 Y + li of accumulator x = 2 X + Y (f32 acc, or the f64 dacc when
-// F64).  FWD0 / FWD: A = h(Z + b), H = h'(Z + b); BWD: delta_{l-1} = H * acc in
-// place; GRAD / GRAD0: the weight gradient into the split's partial slab (GRAD0
-// with the standardisation, column sums cs_col of delta0 in LDS) and, in the
-// tm == 0 tiles, db from the column sum cs of thread t < 64.
-template <int PH, bool F64>
+// the epilogue of a TM x TN output tile (TM = 32 AX, TN = 32 AY; 64 x 64 unless
+// k_gx_gemm_x3 says otherwise): lane holds rows ar + 16 X + 4 lq + y and columns
+// bc + 16 Y + li of accumulator x = AY X + Y (f32 acc, or the f64 dacc when F64).
+// FWD0 / FWD: A = h(Z + b), H = h'(Z + b); BWD: delta_{l-1} = H * acc in place;
+// GRAD / GRAD0: the weight gradient into the split's partial slab (GRAD0 with the
+// standardisation, column sums cs_col of delta0 in LDS) and, in the tm == 0 tiles,
+// db from the column sum cs of thread t < TN.
+template <int PH, bool F64, int AX = 2, int AY = 2>
 __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev& bd, float* S, int l, int tm, int tn,
-                                            int split, int wi, int wo, int ar, int bc, int li, int lq, const v4f (&acc)[4],
-                                            const double (&dacc)[4][4], double cs, const double* cs_col,
-                                            bool lazy = false, double cs2 = 0.0, const float* pre = nullptr) {
+                                            int split, int wi, int wo, int ar, int bc, int li, int lq,
+                                            const v4f (&acc)[AX * AY], const double (&dacc)[AX * AY][4], double cs,
+                                            const double* cs_col, bool lazy = false, double cs2 = 0.0,
+                                            const float* pre = nullptr) {
+  constexpr int TM = 32 * AX, TN = 32 * AY;
   const int t = threadIdx.x;
+  const int64_t rmax = gx_rows(st);  // FWD / BWD: rows past the last tile (TM = 128) are not written
   if constexpr (PH == GX_FWD0 || PH == GX_FWD) {
     const int lay = PH == GX_FWD0 ? 0 : l;
     const float* bias = S + bd.gx_b[lay];
@@ -237,35 +243,39 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     float* Ho = S + bd.gx_h[lay];
     const int64_t ld = bd.gx_ld[lay];
     // the summary layer (lazy head, k_gx_head): the wave's partial of out = A_s w_out
-    // over its 32 columns, per row
+    // over its TN / 2 columns, per row
     const bool head = PH == GX_FWD && l == bd.L - 2 && dh_from_a(bd.act);
     const float* wout = S + bd.gx_w[bd.L - 1];
-    float po[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    // the lane's two columns' bias and w_out (pre: loaded by the caller before its K loop)
-    float bq[2], wq[2];
+    float po[AX][4];
 #pragma unroll
-    for (int Y = 0; Y < 2; ++Y) {
-      const int j = 64 * tn + bc + 16 * Y + li;
+    for (int X = 0; X < AX; ++X) po[X][0] = po[X][1] = po[X][2] = po[X][3] = 0.f;
+    // the lane's columns' bias and w_out (pre: loaded by the caller before its K loop)
+    float bq[AY], wq[AY];
+#pragma unroll
+    for (int Y = 0; Y < AY; ++Y) {
+      const int j = TN * tn + bc + 16 * Y + li;
       bq[Y] = pre ? pre[Y] : (j < wo ? bias[j] : 0.f);
-      wq[Y] = pre ? pre[2 + Y] : (head && j < wo ? wout[j] : 0.f);
+      wq[Y] = pre ? pre[AY + Y] : (head && j < wo ? wout[j] : 0.f);
     }
     // the activation as a compile-time kind (activations.h)
     auto out = [&](auto kind) {
       constexpr int ACT = decltype(kind)::value;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const int j = 64 * tn + bc + 16 * (x & 1) + li;
+      for (int x = 0; x < AX * AY; ++x) {
+        const int X = x / AY, Y = x % AY;
+        const int j = TN * tn + bc + 16 * Y + li;
         if (j >= wo) continue;
-        const float bj = bq[x & 1];
-        const float wj = wq[x & 1];
+        const float bj = bq[Y];
+        const float wj = wq[Y];
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+          const int64_t row = TM * (int64_t)tm + ar + 16 * X + 4 * lq + y;
+          if (TM > 64 && row >= rmax) continue;
           const float z = (F64 ? (float)dacc[x][y] : acc[x][y]) + bj;  // mid_layer_pre_activation: matmul + bias
           const float a = ACT == 0 ? fast_tanh(z) : act_h_t<ACT>(z);  // tanh to ~2 ulp (layer outputs feed GEMMs)
           Ao[row * ld + j] = a;
           if constexpr (ACT == 3) Ho[row * ld + j] = act_dh_t<ACT>(z, a);
-          po[x >> 1][y] += a * wj;  // columns 16 (x & 1) + li: Y = 0 then 1
+          po[X][y] += a * wj;  // columns 16 Y + li, Y in order
         }
       }
     };
@@ -276,11 +286,10 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
       case 3: out(std::integral_constant<int, 3>{}); break;
       default: out(std::integral_constant<int, 4>{}); break;
     }
-    if (head) {  // fixed butterfly over the 16 column lanes; lane li = 0 writes slot 2 tn + (bc / 32)
-      const int64_t rows = gx_rows(st);
-      float* op = S + bd.gx_op + (int64_t)(2 * tn + (bc >> 5)) * rows;
+    if (head) {  // fixed butterfly over the 16 column lanes; lane li = 0 writes slot 2 tn + (column half)
+      float* op = S + bd.gx_op + (int64_t)(2 * tn + (bc != 0 ? 1 : 0)) * rmax;
 #pragma unroll
-      for (int X = 0; X < 2; ++X)
+      for (int X = 0; X < AX; ++X)
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
           float v = po[X][y];
@@ -288,7 +297,8 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
           v += dpp_f<0x4E>(v);   // quad_perm [2, 3, 0, 1]
           v += dpp_f<0x141>(v);  // row_half_mirror
           v += dpp_f<0x140>(v);  // row_mirror: every lane of the 16 holds the same sum
-          if (li == 0) op[64 * (int64_t)tm + ar + 16 * X + 4 * lq + y] = v;
+          const int64_t row = TM * (int64_t)tm + ar + 16 * X + 4 * lq + y;
+          if (li == 0 && (TM == 64 || row < rmax)) op[row] = v;
         }
     }
   } else if constexpr (PH == GX_BWD) {
@@ -298,15 +308,17 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     const int act = bd.act;
     const bool fa = dh_from_a(act);
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+    for (int x = 0; x < AX * AY; ++x) {
+      const int X = x / AY, Y = x % AY;
+      const int j = TN * tn + bc + 16 * Y + li;
       if (j >= wo) continue;
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
-        const int64_t row = 64 * (int64_t)tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        const int64_t row = TM * (int64_t)tm + ar + 16 * X + 4 * lq + y;
+        if (TM > 64 && row >= rmax) continue;
         const float h = fa ? act_dh_a(Ad[row * ld + j], act) : Hd[row * ld + j];
         // delta = h'(z) * (delta_next W^T); lazy head: the accumulator lacks e of the row
-        Hd[row * ld + j] = h * (lazy ? pre[4 * (x >> 1) + y] * acc[x][y] : acc[x][y]);
+        Hd[row * ld + j] = h * (lazy ? pre[4 * X + y] * acc[x][y] : acc[x][y]);
       }
     }
   } else {
@@ -314,25 +326,26 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     const int lay = PH == GX_GRAD ? l : 0;
     const int win = bd.win[lay];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int j = 64 * tn + bc + 16 * (x & 1) + li;
+    for (int x = 0; x < AX * AY; ++x) {
+      const int X = x / AY, Y = x % AY;
+      const int j = TN * tn + bc + 16 * Y + li;
       if (j >= wo) continue;
 #pragma unroll
       for (int y = 0; y < 4; ++y) {
-        const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
+        const int i = TM * tm + ar + 16 * X + 4 * lq + y;
         if (i >= wi) continue;
         double v = dacc[x][y];
-        if (PH == GX_GRAD && lazy) v *= (double)pre[x & 1];  // lazy head: times w_out of the column
+        if (PH == GX_GRAD && lazy) v *= (double)pre[Y];  // lazy head: times w_out of the column
         if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
           const float sg = st.sigma[bd.mk_off + i];
-          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_col[bc + 16 * (x & 1) + li]) / (double)sg : 0.0;
+          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_col[bc + 16 * Y + li]) / (double)sg : 0.0;
         }
         part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
       }
     }
-    if (tm == 0 && t < GX_T && 64 * tn + t < wo) {
-      part[bd.boff[lay] + 64 * tn + t] = (float)cs;                // db_l
-      if (lazy) part[bd.woff[bd.L - 1] + 64 * tn + t] = (float)cs2;  // dW_out = A_s^T e (lazy head)
+    if (tm == 0 && t < TN && TN * tn + t < wo) {
+      part[bd.boff[lay] + TN * tn + t] = (float)cs;                // db_l
+      if (lazy) part[bd.woff[bd.L - 1] + TN * tn + t] = (float)cs2;  // dW_out = A_s^T e (lazy head)
     }
   }
 }
@@ -775,53 +788,61 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
 // accumulation inside a K block, f64 across blocks where K is long (GRAD: the
 // rows).  BANN_GX_EXACT=1 keeps k_gx_gemm (f32 MFMA) for every phase.
 // ---------------------------------------------------------------------------
-#define GX_KB 32    // K block depth
-#define GX_RK 40    // [row][k] stride (bf16 elements): 80-byte rows, conflict-free 16-byte reads
-#define GX_KR 72    // [k][row] stride (bf16 elements), as GX_LDH
-#define GX_PL 2560  // elements per plane: max(64 x GX_RK, GX_KB x GX_KR)
+#define GX_KB 32  // K block depth
+#define GX_RK 40  // [row][k] stride (bf16 elements): 80-byte rows, conflict-free 16-byte reads
 
 namespace {
-// a 64 (MFMA rows) x 32 (K) block of an f32 matrix, 2 x 4 consecutive elements per
-// thread.  RK: M[r][k], thread e = t + 256 u holds row e >> 3, k 4 (e & 7) .. +3.
-// KR: M[k][r], thread e holds k e >> 4, rows 4 (e & 15) .. +3.  Elements outside
-// r < rmax, k < kmax are 0 (masked at the store, as blk_fix).
+// LDS geometry of a staged operand block of R (MFMA) rows x 32 K as three bf16 planes:
+// [row][k] rows of GX_RK, or [k][row] rows of KRS = R + 8 (+ 64 at R = 128: a
+// row stride of 36 dwords mod 64 keeps the ds_read_b64_tr_b16 pairs conflict-free)
+template <int R, bool RK>
+struct Geo {
+  static constexpr int KRS = R == 64 ? 72 : 200;
+  static constexpr int PL = RK ? R * GX_RK : GX_KB * KRS;  // elements per plane
+};
+// an R (MFMA rows) x 32 (K) block of an f32 matrix, R / 32 x 4 consecutive elements
+// per thread.  RK: M[r][k], thread e = t + 256 u holds row e >> 3, k 4 (e & 7) .. +3.
+// KR: M[k][r], thread e holds k e / (R / 4), rows 4 (e % (R / 4)) .. +3.  Elements
+// outside r < rmax, k < kmax are 0 (masked at the store, as blk_fix).
+template <int R>
 struct Blk2 {
-  v4f v[2];
+  v4f v[R / 32];
 };
 struct Blk2Bounds {
   int64_t r0, rmax, k0, kmax;
 };
-template <bool RK>
+template <bool RK, int R>
 __device__ __forceinline__ int blk2_nv(const Blk2Bounds& k, int u) {
   const int e = threadIdx.x + 256 * u;
   if constexpr (RK) {
     const int64_t r = k.r0 + (e >> 3), c = k.k0 + 4 * (e & 7);
     return r < k.rmax ? (int)min(max(k.kmax - c, (int64_t)0), (int64_t)4) : 0;
   } else {
-    const int64_t kk = k.k0 + (e >> 4), r = k.r0 + 4 * (e & 15);
+    const int64_t kk = k.k0 + e / (R / 4), r = k.r0 + 4 * (e % (R / 4));
     return kk < k.kmax ? (int)min(max(k.rmax - r, (int64_t)0), (int64_t)4) : 0;
   }
 }
-template <bool RK>
-__device__ __forceinline__ void blk2_load(Blk2& s, const float* __restrict__ M, int64_t ld, const Blk2Bounds& k) {
+template <bool RK, int R>
+__device__ __forceinline__ void blk2_load(Blk2<R>& s, const float* __restrict__ M, int64_t ld, const Blk2Bounds& k) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < R / 32; ++u) {
     const int e = threadIdx.x + 256 * u;
     v4f x = {0.f, 0.f, 0.f, 0.f};
-    if (blk2_nv<RK>(k, u) > 0)
+    if (blk2_nv<RK, R>(k, u) > 0)
       x = RK ? *(const v4f*)(M + (k.r0 + (e >> 3)) * ld + k.k0 + 4 * (e & 7))    // rows padded to 4
-             : *(const v4f*)(M + (k.k0 + (e >> 4)) * ld + k.r0 + 4 * (e & 15));
+             : *(const v4f*)(M + (k.k0 + e / (R / 4)) * ld + k.r0 + 4 * (e % (R / 4)));
     s.v[u] = x;
   }
 }
-// mask, split into the three planes P[3][GX_PL] and store; csp (KR only) += the
+// mask, split into the three planes P[3][PL] and store; csp (KR only) += the
 // masked values per row of the thread's four
-template <bool RK, bool CS>
-__device__ __forceinline__ void blk2_store(Blk2& s, const Blk2Bounds& k, __bf16* P, double (&csp)[4]) {
+template <bool RK, bool CS, int R>
+__device__ __forceinline__ void blk2_store(Blk2<R>& s, const Blk2Bounds& k, __bf16* P, double (&csp)[4]) {
+  constexpr int PL = Geo<R, RK>::PL, KRS = Geo<R, RK>::KRS;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < R / 32; ++u) {
     const int e = threadIdx.x + 256 * u;
-    const int nv = blk2_nv<RK>(k, u);
+    const int nv = blk2_nv<RK, R>(k, u);
     v4f x = s.v[u];
     if (nv < 1) x.x = 0.f;
     if (nv < 2) x.y = 0.f;
@@ -837,40 +858,48 @@ __device__ __forceinline__ void blk2_store(Blk2& s, const Blk2Bounds& k, __bf16*
       l4[c] = ll;
       if constexpr (CS) csp[c] += (double)x[c];
     }
-    const int off = RK ? (e >> 3) * GX_RK + 4 * (e & 7) : (e >> 4) * GX_KR + 4 * (e & 15);
+    const int off = RK ? (e >> 3) * GX_RK + 4 * (e & 7) : (e / (R / 4)) * KRS + 4 * (e % (R / 4));
     *(bf16x4*)&P[off] = h4;
-    *(bf16x4*)&P[GX_PL + off] = m4;
-    *(bf16x4*)&P[2 * GX_PL + off] = l4;
+    *(bf16x4*)&P[PL + off] = m4;
+    *(bf16x4*)&P[2 * PL + off] = l4;
   }
 }
 // the bf16x8 fragment (MFMA rows rb .. rb + 15, K slots 8 lq .. 8 lq + 7) of plane pl
-template <bool RK>
+template <bool RK, int R>
 __device__ __forceinline__ bf16x8 frag3(const __bf16* P, int pl, int rb, int li, int lq) {
+  constexpr int PL = Geo<R, RK>::PL, KRS = Geo<R, RK>::KRS;
   if constexpr (RK) {
-    return *(const bf16x8*)&P[pl * GX_PL + (rb + li) * GX_RK + 8 * lq];
+    return *(const bf16x8*)&P[pl * PL + (rb + li) * GX_RK + 8 * lq];
   } else {
     const int tq = li >> 2, tp = li & 3;
-    return tr16_pair(&P[pl * GX_PL + (8 * lq + tq) * GX_KR + rb + 4 * tp],
-                     &P[pl * GX_PL + (8 * lq + 4 + tq) * GX_KR + rb + 4 * tp]);
+    return tr16_pair(&P[pl * PL + (8 * lq + tq) * KRS + rb + 4 * tp],
+                     &P[pl * PL + (8 * lq + 4 + tq) * KRS + rb + 4 * tp]);
   }
 }
 }  // namespace
 
-#if GX_ABL & 8  // profiling build: two LDS stages (one barrier per K block, 2 workgroups per CU)
-#define GX_X3_NB 2
-#else
-#define GX_X3_NB 1
-#endif
+// tile shape of k_gx_gemm_x3 per phase: wave tiles of 16 AX x 16 AY, 2 x 2 waves.
+// FWD takes 64 x 128 tiles: its A block (activations, split into planes while
+// staging) feeds twice the MFMAs of a 64 x 64 tile, 3 workgroups per CU (c3def
+// FWD1: 2.78 -> 2.50 ms per 40-branch group).  Measured and not kept: 128 x 128
+// (2 per CU: FWD 2.59, BWD 3.16 -> 3.59 ms), BWD at 64 x 128 (3.17: flat).
+// gx_tiles and the head's slot count follow these.
 template <int PH>
-__global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 4))
+struct X3Shape {
+  static constexpr int AX = 2, AY = PH == GX_FWD ? 4 : 2;
+};
+template <int PH>
+__global__ void __launch_bounds__(256, PH == GX_FWD || PH == GX_GRAD ? 3 : 4)
     k_gx_gemm_x3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
                  int total, int per) {
+  constexpr int AX = X3Shape<PH>::AX, AY = X3Shape<PH>::AY, TM = 32 * AX, TN = 32 * AY;
   constexpr bool ARK = PH != GX_GRAD;  // A staged [row][k]
   constexpr bool BRK = PH == GX_FWD;   // B staged [row][k]
   constexpr bool F64 = PH == GX_GRAD;
-  __shared__ __attribute__((aligned(16))) __bf16 As_[GX_X3_NB][3 * GX_PL];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs_[GX_X3_NB][3 * GX_PL];
-  __shared__ double cs_s[PH == GX_GRAD ? 16 : 1][GX_T];  // GRAD's column sums only
+  constexpr int PLA = Geo<TM, ARK>::PL, PLB = Geo<TN, BRK>::PL, KRSB = Geo<TN, BRK>::KRS;
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * PLA];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PLB];
+  __shared__ double cs_s[PH == GX_GRAD ? 1024 / TN : 1][TN];  // GRAD's column sums only
   const int q = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // XCD-aware numbering (k_gx_gemm)
   if (q >= total) return;
   int lo_ = 0, hi_ = nb;
@@ -882,7 +911,7 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
   const int b = blist[lo_];
   const BranchDev& bd = st.br[b];
   int tmc, tnc, ns;
-  gx_dims(st, bd, PH, l, tmc, tnc, ns);
+  gx_dims(st, bd, PH, l, tmc, tnc, ns, TM, TN);
   int r = q - prefix[lo_];
   const int split = r / (tmc * tnc);
   r -= split * tmc * tnc;
@@ -891,10 +920,12 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
   float* S = gx_base(st, bd);
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int li = lane & 15, lq = lane >> 4;
-  const int ar = 32 * (wv >> 1), bc = 32 * (wv & 1);
-  // lazy head (k_gx_head): delta_s = h'(A_s) * (e w_out) is formed while staging
-  // from A_s, the error e and w_out instead of being stored; GRAD_s's column sums
-  // also give dW_out = A_s^T e
+  const int ar = (TM / 2) * (wv >> 1), bc = (TN / 2) * (wv & 1);
+  // lazy head (k_gx_head): delta_s = h'(A_s) * e * w_out is never stored.  BWD_s:
+  // A = h'(A_s), B = the w_out-scaled planes of Wp_s (k_gx_prep), the epilogue
+  // multiplies row i by e_i; GRAD_s: B = h'(A_s) * e (e of the block's rows, per K
+  // block), the epilogue multiplies column j by w_out_j; its column sums give db_s
+  // (times w_out) and dW_out = A_s^T e (f64, from the raw A_s values)
   const bool lazy = PH != GX_FWD && l == bd.L - 2 && dh_from_a(bd.act);
   const float* ev = S + bd.gx_e;
   const float* wout = S + bd.gx_w[bd.L - 1];
@@ -931,134 +962,139 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     kb1 = 2 * ((int64_t)ntile * (split + 1) / ns);
   }
   if constexpr (PH != GX_GRAD) kb1 = (kcount + GX_KB - 1) / GX_KB;
-  // the operand blocks of K block kb: rows of the A block are output rows (64 tm ..),
-  // rows of the B block output columns (64 tn ..)
+  // the operand blocks of K block kb: rows of the A block are output rows (TM tm ..),
+  // rows of the B block output columns (TN tn ..)
   auto bnd_a = [&](int64_t kb) {
-    return Blk2Bounds{64 * (int64_t)tm, PH == GX_GRAD ? (int64_t)wi : rows, GX_KB * kb, kcount};
+    return Blk2Bounds{TM * (int64_t)tm, PH == GX_GRAD ? (int64_t)wi : rows, GX_KB * kb, kcount};
   };
-  auto bnd_b = [&](int64_t kb) { return Blk2Bounds{64 * (int64_t)tn, (int64_t)wo, GX_KB * kb, kcount}; };
-  Blk2 ra, rb;
+  auto bnd_b = [&](int64_t kb) { return Blk2Bounds{TN * (int64_t)tn, (int64_t)wo, GX_KB * kb, kcount}; };
+  Blk2<TM> ra;
+  Blk2<TN> rb;
   double csa[4] = {0.0, 0.0, 0.0, 0.0}, csp[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD: column sums of delta_l
-  // FWD / BWD: B = Wp_l from its pre-split planes [3][out][r32(in)] (k_gx_prep): one
-  // 16-byte piece of 8 elements per plane and thread, copied to the stage as is.
-  // FWD stages it [out][in] (thread: out row t >> 2, in 8 (t & 3) ..), BWD [out = k][in]
-  // (thread: out row t >> 3, in 8 (t & 7) ..); rows past the layer and pieces past
-  // the in width are zero (the planes' padding covers the rest of a piece)
+  // FWD / BWD: B = Wp_l from its pre-split planes [3][out][r32(in)] (k_gx_prep): TN / 64
+  // 16-byte pieces of 8 elements per plane and thread, copied to the stage as is.
+  // FWD stages it [out][in] (piece p: out row p >> 2, in 8 (p & 3) ..), BWD [out = k][in]
+  // (piece p: out row p / (TN / 8), in 8 (p % (TN / 8)) ..); rows past the layer and
+  // pieces past the in width are zero (the planes' padding covers the rest of a piece)
   constexpr bool BP = PH != GX_GRAD;
-  v4i rbp[3];
+  constexpr int NP = TN / 64;
+  v4i rbp[NP][3];
   const __bf16* Wp3 = BP ? reinterpret_cast<const __bf16*>(S + (PH == GX_BWD && lazy ? bd.gx_wps : bd.gx_wp[l]))
                          : nullptr;
   const int64_t l3 = BP ? ((bd.win[l] + 31) & ~31) : 0, p3 = BP ? (int64_t)bd.widths[l] * l3 : 0;
-  auto load_bp = [&](v4i (&rp_)[3], int64_t kb) {
-    int64_t row, col;
-    bool ok;
-    if constexpr (PH == GX_FWD) {
-      row = 64 * (int64_t)tn + (t >> 2);
-      col = GX_KB * kb + 8 * (t & 3);
-      ok = row < wo;
-    } else {
-      row = GX_KB * kb + (t >> 3);
-      col = 64 * (int64_t)tn + 8 * (t & 7);
-      ok = row < kcount && col < wo;
+  auto load_bp = [&](int64_t kb) {
+#pragma unroll
+    for (int v = 0; v < NP; ++v) {
+      const int pc = t + 256 * v;
+      int64_t row, col;
+      bool ok;
+      if constexpr (PH == GX_FWD) {
+        row = TN * (int64_t)tn + (pc >> 2);
+        col = GX_KB * kb + 8 * (pc & 3);
+        ok = row < wo;
+      } else {
+        row = GX_KB * kb + pc / (TN / 8);
+        col = TN * (int64_t)tn + 8 * (pc % (TN / 8));
+        ok = row < kcount && col < wo;
+      }
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        rbp[v][pl] = ok ? *reinterpret_cast<const v4i*>(Wp3 + pl * p3 + row * l3 + col) : v4i{0, 0, 0, 0};
     }
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-      rp_[pl] = ok ? *reinterpret_cast<const v4i*>(Wp3 + pl * p3 + row * l3 + col) : v4i{0, 0, 0, 0};
   };
-  auto store_bp = [&](v4i (&rp_)[3], __bf16* Bs) {
-    const int off = PH == GX_FWD ? (t >> 2) * GX_RK + 8 * (t & 3) : (t >> 3) * GX_KR + 8 * (t & 7);
+  auto store_bp = [&]() {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<v4i*>(&Bs[pl * GX_PL + off]) = rp_[pl];
+    for (int v = 0; v < NP; ++v) {
+      const int pc = t + 256 * v;
+      const int off = PH == GX_FWD ? (pc >> 2) * GX_RK + 8 * (pc & 3) : (pc / (TN / 8)) * KRSB + 8 * (pc % (TN / 8));
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<v4i*>(&Bs[pl * PLB + off]) = rbp[v][pl];
+    }
   };
   const bool want_cs = PH == GX_GRAD && tm == 0;
 
-  v4f acc[4];
-  double dacc[4][4];
+  v4f acc[AX * AY];
+  double dacc[AX * AY][4];
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
+  for (int x = 0; x < AX * AY; ++x) {
     acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int y = 0; y < 4; ++y) dacc[x][y] = 0.0;
   }
-  // lazy head: delta_s = h'(A_s) * e * w_out is never stored.  BWD_s: A = h'(A_s),
-  // B = the w_out-scaled planes of Wp_s (k_gx_prep), the epilogue multiplies row i
-  // by e_i; GRAD_s: B = h'(A_s) * e (e of the block's rows, per K block), the
-  // epilogue multiplies column j by w_out_j; its column sums give db_s (times w_out)
-  // and dW_out = A_s^T e (f64, from the raw A_s values)
-  float le[2] = {0.f, 0.f};
+  float le[4] = {0.f, 0.f, 0.f, 0.f};
   double csq[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD_s, tm == 0: dW_out column sums
   auto lazy_load = [&](int64_t kb) {
     if constexpr (PH == GX_GRAD) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) le[u] = ev[GX_KB * kb + ((t + 256 * u) >> 4)];
+      for (int u = 0; u < 2; ++u) le[u] = ev[GX_KB * kb + (t + 256 * u) / (TN / 4)];
     }
   };
   const DhA dk = dh_a_consts(bd.act);
   const bool tanh_act = bd.act == 0;
-  auto lazy_h = [&](Blk2& r) {  // r = h'(A_s) (* e of the row: GRAD)
+  auto lazy_h = [&](auto& rr) {  // rr = h'(A_s) (* e of the row: GRAD)
+    constexpr int NU = sizeof(rr.v) / sizeof(v4f);
     if (tanh_act) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float a = r.v[u][c];
-          r.v[u][c] = PH == GX_GRAD ? (1.f - a * a) * le[u] : 1.f - a * a;
+          const float a = rr.v[u][c];
+          rr.v[u][c] = PH == GX_GRAD ? (1.f - a * a) * le[u] : 1.f - a * a;
         }
     } else {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < NU; ++u)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float h = dh_a(r.v[u][c], dk);
-          r.v[u][c] = PH == GX_GRAD ? h * le[u] : h;
+          const float h = dh_a(rr.v[u][c], dk);
+          rr.v[u][c] = PH == GX_GRAD ? h * le[u] : h;
         }
     }
   };
-  auto lazy_dwo = [&](const Blk2& r) {
+  auto lazy_dwo = [&](const Blk2<TN>& rr) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < TN / 32; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) csq[c] += (double)r.v[u][c] * (double)le[u];
+      for (int c = 0; c < 4; ++c) csq[c] += (double)rr.v[u][c] * (double)le[u];
   };
   // values the epilogue needs, loaded before the K loop (gx_epilogue): FWD the bias
-  // and w_out of the lane's two columns, lazy BWD_s the e of its eight rows, lazy
-  // GRAD_s w_out of its two columns
-  float pre[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // and w_out of the lane's AY columns, lazy BWD_s the e of its 4 AX rows, lazy
+  // GRAD_s w_out of its AY columns
+  float pre[4 * AX > 2 * AY ? 4 * AX : 2 * AY];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(pre) / sizeof(float)); ++i) pre[i] = 0.f;
   if constexpr (PH == GX_FWD) {
     const bool head = l == bd.L - 2 && dh_from_a(bd.act);
 #pragma unroll
-    for (int Y = 0; Y < 2; ++Y) {
-      const int j = 64 * tn + bc + 16 * Y + li;
+    for (int Y = 0; Y < AY; ++Y) {
+      const int j = TN * tn + bc + 16 * Y + li;
       pre[Y] = j < wo ? S[bd.gx_b[l] + j] : 0.f;
-      pre[2 + Y] = head && j < wo ? wout[j] : 0.f;
+      pre[AY + Y] = head && j < wo ? wout[j] : 0.f;
     }
   } else if constexpr (PH == GX_BWD) {
     if (lazy)
 #pragma unroll
-      for (int X = 0; X < 2; ++X)
+      for (int X = 0; X < AX; ++X)
 #pragma unroll
-        for (int y = 0; y < 4; ++y) pre[4 * X + y] = ev[64 * (int64_t)tm + ar + 16 * X + 4 * lq + y];
+        for (int y = 0; y < 4; ++y) {
+          const int64_t row = TM * (int64_t)tm + ar + 16 * X + 4 * lq + y;
+          pre[4 * X + y] = row < rows ? ev[row] : 0.f;
+        }
   } else {
     if (lazy)
 #pragma unroll
-      for (int Y = 0; Y < 2; ++Y) {
-        const int j = 64 * tn + bc + 16 * Y + li;
+      for (int Y = 0; Y < AY; ++Y) {
+        const int j = TN * tn + bc + 16 * Y + li;
         pre[Y] = j < wo ? wout[j] : 0.f;
       }
   }
   auto load = [&](int64_t kb) {
     if (lazy) lazy_load(kb);
-#if !(GX_ABL & 2)
-    blk2_load<ARK>(ra, Am, lda, bnd_a(kb));
-#endif
-#if !(GX_ABL & 1)
-    if constexpr (BP) load_bp(rbp, kb);
-    else blk2_load<BRK>(rb, Bm, ldb, bnd_b(kb));
-#endif
+    blk2_load<ARK, TM>(ra, Am, lda, bnd_a(kb));
+    if constexpr (BP) load_bp(kb);
+    else blk2_load<BRK, TN>(rb, Bm, ldb, bnd_b(kb));
   };
-  auto stage = [&](int64_t kb, int buf) {
-    __bf16* As = As_[buf];
-    __bf16* Bs = Bs_[buf];
+  auto stage = [&](int64_t kb) {
     if constexpr (PH == GX_BWD) {
       if (lazy) lazy_h(ra);
     } else if constexpr (PH == GX_GRAD) {
@@ -1067,35 +1103,25 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
         lazy_h(rb);
       }
     }
-#if !(GX_ABL & 2)  // profiling builds: GX_ABL 1 / 2 skip the B / A staging, 4 the MFMAs
-    blk2_store<ARK, false>(ra, bnd_a(kb), As, csa);
-#endif
-#if !(GX_ABL & 1)
-    if constexpr (BP) store_bp(rbp, Bs);
-    else if (want_cs) blk2_store<BRK, true>(rb, bnd_b(kb), Bs, csp);
-    else blk2_store<BRK, false>(rb, bnd_b(kb), Bs, csp);
-#endif
+    blk2_store<ARK, false, TM>(ra, bnd_a(kb), As, csa);
+    if constexpr (BP) store_bp();
+    else if (want_cs) blk2_store<BRK, true, TN>(rb, bnd_b(kb), Bs, csp);
+    else blk2_store<BRK, false, TN>(rb, bnd_b(kb), Bs, csp);
   };
-  auto compute = [&](int64_t kb, int buf) {
-    const __bf16* As = As_[buf];
-    const __bf16* Bs = Bs_[buf];
-    bf16x8 a[2][3];
+  auto compute = [&](int64_t kb) {
+    bf16x8 a[AX][3];
 #pragma unroll
-    for (int X = 0; X < 2; ++X)
+    for (int X = 0; X < AX; ++X)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[X][pl] = frag3<ARK>(As, pl, ar + 16 * X, li, lq);
+      for (int pl = 0; pl < 3; ++pl) a[X][pl] = frag3<ARK, TM>(As, pl, ar + 16 * X, li, lq);
 #pragma unroll
-    for (int Y = 0; Y < 2; ++Y) {
+    for (int Y = 0; Y < AY; ++Y) {
       bf16x8 bq[3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) bq[pl] = frag3<BRK>(Bs, pl, bc + 16 * Y, li, lq);
+      for (int pl = 0; pl < 3; ++pl) bq[pl] = frag3<BRK, TN>(Bs, pl, bc + 16 * Y, li, lq);
 #pragma unroll
-      for (int X = 0; X < 2; ++X) {
-        v4f& c = acc[2 * X + Y];
-#if GX_ABL & 4
-        c += v4f{(float)a[X][2][0], (float)bq[0][1], (float)a[X][0][3], (float)bq[2][5]};
-        continue;
-#endif
+      for (int X = 0; X < AX; ++X) {
+        v4f& c = acc[AY * X + Y];
         // small products first
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][2], bq[0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[X][1], bq[1], c, 0, 0, 0);
@@ -1108,7 +1134,7 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     if constexpr (F64) {
       if (kb & 1) {  // f64 across 64-deep K
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
+        for (int x = 0; x < AX * AY; ++x) {
           dacc[x][0] += (double)acc[x].x;
           dacc[x][1] += (double)acc[x].y;
           dacc[x][2] += (double)acc[x].z;
@@ -1119,33 +1145,16 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     }
   };
   if (kb0 < kb1) load(kb0);
-  if constexpr (GX_X3_NB == 1) {
-    for (int64_t kb = kb0; kb < kb1; ++kb) {
-      stage(kb, 0);
-      __syncthreads();
-      if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
-      compute(kb, 0);
-      __syncthreads();  // every wave is done with the stage before it is refilled
-    }
-  } else {  // stage kb + 1 into the other buffer while kb computes: one barrier per block
-    if (kb0 < kb1) {
-      stage(kb0, 0);
-      if (kb0 + 1 < kb1) load(kb0 + 1);
-      __syncthreads();
-    }
-    for (int64_t kb = kb0; kb < kb1; ++kb) {
-      const int buf = (int)((kb - kb0) & 1);
-      compute(kb, buf);
-      if (kb + 1 < kb1) {
-        stage(kb + 1, buf ^ 1);
-        if (kb + 2 < kb1) load(kb + 2);
-      }
-      __syncthreads();
-    }
+  for (int64_t kb = kb0; kb < kb1; ++kb) {
+    stage(kb);
+    __syncthreads();
+    if (kb + 1 < kb1) load(kb + 1);  // lands during this block's MFMAs
+    compute(kb);
+    __syncthreads();  // every wave is done with the stage before it is refilled
   }
   if constexpr (F64) {  // an odd block count leaves one block in acc
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
+    for (int x = 0; x < AX * AY; ++x) {
       dacc[x][0] += (double)acc[x].x;
       dacc[x][1] += (double)acc[x].y;
       dacc[x][2] += (double)acc[x].z;
@@ -1153,24 +1162,25 @@ __global__ void __launch_bounds__(256, GX_X3_NB == 2 ? 2 : (PH == GX_GRAD ? 3 : 
     }
   }
   double cs = 0.0, cs2 = 0.0;
-  if (want_cs) {  // 16 threads per 4-column group, added in thread order (deterministic)
+  if (want_cs) {  // 1024 / TN threads per 4-column group, added in thread order (deterministic)
+    constexpr int RW = TN / 4;
 #pragma unroll
-    for (int x = 0; x < 4; ++x) cs_s[t >> 4][4 * (t & 15) + x] = csp[x];
+    for (int x = 0; x < 4; ++x) cs_s[t / RW][4 * (t % RW) + x] = csp[x];
     __syncthreads();
-    if (t < GX_T)
-      for (int k = 0; k < 16; ++k) cs += cs_s[k][t];
+    if (t < TN)
+      for (int k = 0; k < 1024 / TN; ++k) cs += cs_s[k][t];
     if (lazy) {  // db_s = w_out * (column sums of h'(A_s) e); the dW_out column sums, same order
-      cs *= (t < GX_T && 64 * tn + t < wo) ? (double)wout[64 * tn + t] : 0.0;
+      cs *= (t < TN && TN * tn + t < wo) ? (double)wout[TN * tn + t] : 0.0;
       __syncthreads();
 #pragma unroll
-      for (int x = 0; x < 4; ++x) cs_s[t >> 4][4 * (t & 15) + x] = csq[x];
+      for (int x = 0; x < 4; ++x) cs_s[t / RW][4 * (t % RW) + x] = csq[x];
       __syncthreads();
-      if (t < GX_T)
-        for (int k = 0; k < 16; ++k) cs2 += cs_s[k][t];
+      if (t < TN)
+        for (int k = 0; k < 1024 / TN; ++k) cs2 += cs_s[k][t];
     }
   }
-  gx_epilogue<PH, F64>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, nullptr, lazy, cs2,
-                       PH == GX_FWD || lazy ? pre : nullptr);
+  gx_epilogue<PH, F64, AX, AY>(st, bd, S, l, tm, tn, split, wi, wo, ar, bc, li, lq, acc, dacc, cs, nullptr, lazy, cs2,
+                               PH == GX_FWD || lazy ? pre : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1279,7 +1289,8 @@ __global__ void __launch_bounds__(256) k_gx_head(DevState st, const int32_t* __r
     const int t = threadIdx.x;
     if (t >= GX_T) return;
     const int64_t rows = gx_rows(st), row = 64 * (int64_t)tile + t;
-    const int ns = 2 * ((Sw + 63) / 64);
+    constexpr int TNF = 32 * X3Shape<GX_FWD>::AY;  // the summary layer's FWD tiles (k_gx_gemm_x3)
+    const int ns = 2 * ((Sw + TNF - 1) / TNF);
     const float* op = S + bd.gx_op + row;
     double acc = 0.0;
     for (int k = 0; k < ns; ++k) acc += (double)op[k * rows];
@@ -1413,11 +1424,17 @@ void launch_gx_gemm(const DevState& st, int ph, int l, const int32_t* blist, con
 int64_t gx_tiles(const BranchDev& d, int ph, int l, int32_t nfrag) {
   const int64_t ntile = (nfrag + 3) / 4;
   auto cd = [](int64_t a) { return (a + 63) / 64; };
+  const bool x3 = !gx_exact();  // k_gx_gemm_x3's tile shapes (X3Shape), else 64 x 64
+  const int64_t tmf = x3 ? 32 * X3Shape<GX_FWD>::AX : 64, tnf = x3 ? 32 * X3Shape<GX_FWD>::AY : 64;
+  const int64_t tmb = x3 ? 32 * X3Shape<GX_BWD>::AX : 64, tnb = x3 ? 32 * X3Shape<GX_BWD>::AY : 64;
+  const int64_t tmg = x3 ? 32 * X3Shape<GX_GRAD>::AX : 64, tng = x3 ? 32 * X3Shape<GX_GRAD>::AY : 64;
+  auto c = [](int64_t a, int64_t e) { return (a + e - 1) / e; };
   switch (ph) {
     case GX_FWD0: return ntile * cd(d.widths[0]);
-    case GX_FWD: return (l >= 1 && l < d.L - 1) ? ntile * cd(d.widths[l]) : 0;
-    case GX_BWD: return (l >= 1 && l < d.L - 1) ? ntile * cd(d.widths[l - 1]) : 0;
-    case GX_GRAD: return (l >= 1 && l < d.L - 1) ? cd(d.widths[l - 1]) * cd(d.widths[l]) * d.nsplits : 0;
+    case GX_FWD: return (l >= 1 && l < d.L - 1) ? c(64 * ntile, tmf) * c(d.widths[l], tnf) : 0;
+    case GX_BWD: return (l >= 1 && l < d.L - 1) ? c(64 * ntile, tmb) * c(d.widths[l - 1], tnb) : 0;
+    case GX_GRAD:
+      return (l >= 1 && l < d.L - 1) ? c(d.widths[l - 1], tmg) * c(d.widths[l], tng) * d.nsplits : 0;
     default: return (int64_t)d.nchunks * cd(d.widths[0]) * d.nsplits;
   }
 }
