@@ -227,6 +227,27 @@ __device__ __forceinline__ float act_dh_a(float a, int act) {
 // GRAD / GRAD0: the weight gradient into the split's partial slab (GRAD0 with the
 // standardisation, column sums cs_col of delta0 in LDS) and, in the tm == 0 tiles,
 // db from the column sum cs of thread t < TN.
+// BWD: the h' operands of the lane's outputs (A_{l-1}, or H_{l-1} for SiLU), column
+// and row clamped into the layer (the clamped ones are not used)
+template <int AX, int AY>
+__device__ __forceinline__ void gx_bwd_hload(const DevState& st, const BranchDev& bd, const float* S, int l, int tm,
+                                             int tn, int wo, int ar, int bc, int li, int lq, float* hv) {
+  constexpr int TM = 32 * AX, TN = 32 * AY;
+  const int64_t rmax = gx_rows(st);
+  const float* Hsrc = S + (dh_from_a(bd.act) ? bd.gx_a[l - 1] : bd.gx_h[l - 1]);
+  const int64_t ld = bd.gx_ld[l - 1];
+#pragma unroll
+  for (int x = 0; x < AX * AY; ++x) {
+    const int X = x / AY, Y = x % AY;
+    const int jc = min(TN * tn + bc + 16 * Y + li, wo - 1);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int64_t row = min(TM * (int64_t)tm + ar + 16 * X + 4 * lq + y, rmax - 1);
+      hv[4 * x + y] = Hsrc[row * ld + jc];
+    }
+  }
+}
+
 template <int PH, bool F64, int AX = 2, int AY = 2>
 __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev& bd, float* S, int l, int tm, int tn,
                                             int split, int wi, int wo, int ar, int bc, int li, int lq,
@@ -307,6 +328,12 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     const int64_t ld = bd.gx_ld[l - 1];
     const int act = bd.act;
     const bool fa = dh_from_a(act);
+    // every h' operand is loaded first, unconditionally (gx_bwd_hload), so the loads
+    // issue back to back: one memory latency per tile instead of one per guarded
+    // group (BWD1 at c3def: 3.2 -> 2.9 ms per group).  Measured and not kept: the
+    // same loads issued during the last K block's MFMAs (3.27 ms)
+    float hv[AX * AY][4];
+    gx_bwd_hload<AX, AY>(st, bd, S, l, tm, tn, wo, ar, bc, li, lq, &hv[0][0]);
 #pragma unroll
     for (int x = 0; x < AX * AY; ++x) {
       const int X = x / AY, Y = x % AY;
@@ -316,7 +343,7 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
       for (int y = 0; y < 4; ++y) {
         const int64_t row = TM * (int64_t)tm + ar + 16 * X + 4 * lq + y;
         if (TM > 64 && row >= rmax) continue;
-        const float h = fa ? act_dh_a(Ad[row * ld + j], act) : Hd[row * ld + j];
+        const float h = fa ? act_dh_a(hv[x][y], act) : hv[x][y];
         // delta = h'(z) * (delta_next W^T); lazy head: the accumulator lacks e of the row
         Hd[row * ld + j] = h * (lazy ? pre[4 * X + y] * acc[x][y] : acc[x][y]);
       }
@@ -325,6 +352,18 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
     float* part = st.part + bd.part_off + (int64_t)split * bd.P;
     const int lay = PH == GX_GRAD ? l : 0;
     const int win = bd.win[lay];
+    // GRAD0: sigma and mu of the lane's 4 AX markers, loaded together (index clamped)
+    float sgv[AX][4], muv[AX][4];
+    if constexpr (PH == GX_GRAD0) {
+#pragma unroll
+      for (int X = 0; X < AX; ++X)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int ic = min(TM * tm + ar + 16 * X + 4 * lq + y, wi - 1);
+          sgv[X][y] = st.sigma[bd.mk_off + ic];
+          muv[X][y] = st.mu[bd.mk_off + ic];
+        }
+    }
 #pragma unroll
     for (int x = 0; x < AX * AY; ++x) {
       const int X = x / AY, Y = x % AY;
@@ -337,8 +376,8 @@ __device__ __forceinline__ void gx_epilogue(const DevState& st, const BranchDev&
         double v = dacc[x][y];
         if (PH == GX_GRAD && lazy) v *= (double)pre[Y];  // lazy head: times w_out of the column
         if constexpr (PH == GX_GRAD0) {  // X = (g - mu) / sigma; zero-variance markers contribute 0
-          const float sg = st.sigma[bd.mk_off + i];
-          v = sg > 0.f ? (v - (double)st.mu[bd.mk_off + i] * cs_col[bc + 16 * Y + li]) / (double)sg : 0.0;
+          const float sg = sgv[X][y];
+          v = sg > 0.f ? (v - (double)muv[X][y] * cs_col[bc + 16 * Y + li]) / (double)sg : 0.0;
         }
         part[bd.woff[lay] + (int64_t)j * win + i] = (float)v;  // param_vec: W_l[out j][in i]
       }
@@ -754,6 +793,15 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
     __syncthreads();
     float* part = st.part + bd.part_off + (int64_t)split * bd.P;
     const int wi = bd.m, win = bd.m;
+    float sgv[2][4], muv[2][4];  // the lane's eight markers, loaded together (index clamped)
+#pragma unroll
+    for (int X = 0; X < 2; ++X)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) {
+        const int ic = min(64 * tm + ar + 16 * X + 4 * lq + y, wi - 1);
+        sgv[X][y] = st.sigma[bd.mk_off + ic];
+        muv[X][y] = st.mu[bd.mk_off + ic];
+      }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const int jc = bc + 16 * (x & 1) + li;
@@ -764,8 +812,8 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
       for (int y = 0; y < 4; ++y) {
         const int i = 64 * tm + ar + 16 * (x >> 1) + 4 * lq + y;
         if (i >= wi) continue;
-        const float sg = st.sigma[bd.mk_off + i];
-        const double v = sg > 0.f ? (dacc[x][y] - (double)st.mu[bd.mk_off + i] * cs) / (double)sg : 0.0;
+        const float sg = sgv[x >> 1][y];
+        const double v = sg > 0.f ? (dacc[x][y] - (double)muv[x >> 1][y] * cs) / (double)sg : 0.0;
         part[bd.woff[0] + (int64_t)j * win + i] = (float)v;
       }
     }
