@@ -770,9 +770,16 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   int64_t q_off = 0;
   int64_t x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   // gx scratch groups: branches in index order until the budget (BANN_GX_SCRATCH_MB,
-  // default 8 GiB) is full; every group reuses the same device scratch
+  // default a quarter of the free device memory, at most 64 GiB) is full; every
+  // group reuses the same device scratch.  Fewer, larger groups fill the GPU better
+  // (c3def: 8 GiB = 40 branches per group 335 ms per evaluation, 32 GiB 321 ms)
   const int64_t gx_rows = ntile * 64;
   int64_t gx_budget = 8192ll << 18;  // floats
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 0)
+      gx_budget = std::max<int64_t>(gx_budget, std::min<int64_t>((int64_t)(fr / 4) / 4, 65536ll << 18));
+  }
   if (const char* e = getenv("BANN_GX_SCRATCH_MB")) gx_budget = std::max<int64_t>(1, atoll(e)) << 18;
   int64_t gx_cur = 0, n_gx = 0;
   int32_t gx_ngroups = 0;
