@@ -14,6 +14,7 @@ ap.add_argument("--m", type=int, default=500)
 ap.add_argument("--widths", default="4,4,1")
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--tag", default="")
+ap.add_argument("--forward", type=int, default=0, help="then K forward-only passes (bann_predict_many; time them in a kernel trace)")
 a = ap.parse_args()
 w = [int(x) for x in a.widths.split(",")]
 ctx = BannContext(0)
@@ -34,3 +35,6 @@ xb = ((a.n + 3) // 4) * a.m * a.branches   # 2-bit genotypes (the .bed payload s
 print(json.dumps(dict(tag=a.tag, lib=os.environ.get("BANN_LIB", "default"), branches=a.branches, n=a.n, m=a.m,
                       path=ctx.kernel_path(0), grad_ms=round(g, 4), update_ms=round(u, 4),
                       alg_GBps=round((xb + 4 * a.n * a.branches) / g / 1e6, 1))), flush=True)
+ctx.leapfrog_end()
+for _ in range(a.forward):
+    ctx.predict_many(list(range(a.branches)))
