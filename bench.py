@@ -216,7 +216,7 @@ def main():
     if args.cpu_sample_branches is None:
         args.cpu_sample_branches = 4 if heavy else 96
     if args.cpu_sample_steps is None:
-        args.cpu_sample_steps = 2 if heavy else 16
+        args.cpu_sample_steps = 2 if heavy else 24  # ~10-15 s of CPU work at C3
     m_b = M_total // B_total
     b0, b1 = shard_ranges([m_b] * B_total, max(world, args.emulate_shard))[rank]   # contiguous, balanced by markers
     nb = b1 - b0
