@@ -646,12 +646,17 @@ def test_layered_scratch_groups_and_packing(Ctx):
     """gx branches of mixed shapes in several scratch groups (a 1 MiB budget puts
     every branch in its own group, so later groups overwrite the scratch of
     earlier ones): every gradient matches the oracle, equals the one-group
-    result bitwise, and is bitwise reproducible."""
+    result bitwise, and is bitwise reproducible.  The lazy head (kernels_gx.hip:
+    delta_s formed while BWD_s / GRAD_s stage A_s) runs for tanh, leaky ReLU and
+    identity after one or two hidden layers, beside branches that keep the stored
+    head (SiLU, no hidden layer) in the same group."""
     rng = np.random.default_rng(29)
     n, M = 1500, 900
     g = O.synthetic_genotypes(rng, n, M)
     shapes = [(300, [150, 150, 1], "tanh", "ridge_ard"), (70, [35, 1], "relu", "lasso_base"),
-              (129, [64, 65, 3, 1], "silu", "ridge_base"), (500, [5, 250, 1], "tanh", "lasso_ard")]
+              (129, [64, 65, 3, 1], "silu", "ridge_base"), (500, [5, 250, 1], "tanh", "lasso_ard"),
+              (180, [90, 60, 30, 1], "tanh", "ridge_ard"), (150, [75, 40, 1], "leaky_relu", "ridge_base"),
+              (100, [50, 130, 1], "identity", "lasso_ard")]
     specs = []
     for m, w, a, p in shapes:
         snps = rng.choice(M, size=m, replace=False).astype(np.int32)
