@@ -587,6 +587,9 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? (PH == GX_GRAD ? 3 : 4) : 
 // LDS images [row][k] with 72-element rows (conflict-free 16-byte fragment reads).
 // ---------------------------------------------------------------------------
 #define GX_LDH 72  // bf16 row stride (elements)
+#ifndef GX_F64_EVERY
+#define GX_F64_EVERY 4  // 64-deep K blocks per f32 accumulation before the f64 sum (256 rows / markers)
+#endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
@@ -682,6 +685,7 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
     }
   };
   double csp[4] = {0.0, 0.0, 0.0, 0.0};  // GRAD0: column sums of delta0, columns 4 (t & 15) + x
+  float cspf[4] = {0.f, 0.f, 0.f, 0.f};  //   their f32 part since the last f64 sum (with dacc's)
   auto store = [&](int kb) {
     int jl, dq;
     geno_pos(jl, dq);
@@ -714,7 +718,7 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
           h4[x] = hh;
           m4[x] = mm;
           l4[x] = ll;
-          csp[x] += (double)rb.v[u][x];
+          cspf[x] += rb.v[u][x];
         }
         *(bf16x4*)&Bs[0][rr * GX_LDH + c4] = h4;
         *(bf16x4*)&Bs[1][rr * GX_LDH + c4] = m4;
@@ -765,13 +769,19 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
         acc[3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[3], 0, 0, 0);
       }
     }
+    if (((kb - kb0) & (GX_F64_EVERY - 1)) == GX_F64_EVERY - 1 || kb + 1 == kb1) {  // f64 across 256-deep K
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      dacc[x][0] += (double)acc[x].x;
-      dacc[x][1] += (double)acc[x].y;
-      dacc[x][2] += (double)acc[x].z;
-      dacc[x][3] += (double)acc[x].w;
-      acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+      for (int x = 0; x < 4; ++x) {
+        dacc[x][0] += (double)acc[x].x;
+        dacc[x][1] += (double)acc[x].y;
+        dacc[x][2] += (double)acc[x].z;
+        dacc[x][3] += (double)acc[x].w;
+        acc[x] = v4f{0.f, 0.f, 0.f, 0.f};
+        if constexpr (PH == GX_GRAD0) {
+          csp[x] += (double)cspf[x];
+          cspf[x] = 0.f;
+        }
+      }
     }
     __syncthreads();  // every wave is done with the stage before it is refilled
   }
@@ -1180,7 +1190,7 @@ __global__ void __launch_bounds__(256, PH == GX_FWD || PH == GX_GRAD ? 3 : 4)
       }
     }
     if constexpr (F64) {
-      if (kb & 1) {  // f64 across 64-deep K
+      if ((kb & (2 * GX_F64_EVERY - 1)) == 2 * GX_F64_EVERY - 1) {  // f64 across 256-deep K
 #pragma unroll
         for (int x = 0; x < AX * AY; ++x) {
           dacc[x][0] += (double)acc[x].x;
