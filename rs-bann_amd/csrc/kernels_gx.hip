@@ -594,11 +594,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 namespace {
+// x = hi + mid + lo exactly, by truncation: hi = the top 8 significant bits, mid
+// the next 8 of the (exact) remainder, lo the last 8 (representable as is): two
+// ANDs and two subtractions, no conversions; each plane is the high half of an
+// f32 word
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mi, __bf16& lo) {
-  hi = (__bf16)x;
-  const float r = x - (float)hi;  // exact
-  mi = (__bf16)r;
-  lo = (__bf16)(r - (float)mi);   // exact difference, rounded once
+  const uint32_t hb = __float_as_uint(x) & 0xFFFF0000u;
+  const float r = x - __uint_as_float(hb);  // exact
+  const uint32_t mb = __float_as_uint(r) & 0xFFFF0000u;
+  const uint32_t lb = __float_as_uint(r - __uint_as_float(mb));  // exact, <= 8 significant bits
+  hi = __builtin_bit_cast(__bf16, (uint16_t)(hb >> 16));
+  mi = __builtin_bit_cast(__bf16, (uint16_t)(mb >> 16));
+  lo = __builtin_bit_cast(__bf16, (uint16_t)(lb >> 16));
 }
 }  // namespace
 
