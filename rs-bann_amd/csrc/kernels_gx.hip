@@ -951,10 +951,10 @@ __device__ __forceinline__ bf16x8 frag3(const __bf16* P, int pl, int rb, int li,
 // gx_tiles and the head's slot count follow these.
 template <int PH>
 struct X3Shape {
-  static constexpr int AX = 2, AY = PH == GX_FWD ? 4 : 2;
+  static constexpr int AX = 2, AY = PH == GX_BWD ? 2 : 4;
 };
 template <int PH>
-__global__ void __launch_bounds__(256, PH == GX_FWD || PH == GX_GRAD ? 3 : 4)
+__global__ void __launch_bounds__(256, PH == GX_FWD ? 3 : (PH == GX_GRAD ? 2 : 4))
     k_gx_gemm_x3(DevState st, const int32_t* __restrict__ blist, const int32_t* __restrict__ prefix, int nb, int l,
                  int total, int per) {
   constexpr int AX = X3Shape<PH>::AX, AY = X3Shape<PH>::AY, TM = 32 * AX, TN = 32 * AY;
@@ -1091,7 +1091,7 @@ __global__ void __launch_bounds__(256, PH == GX_FWD || PH == GX_GRAD ? 3 : 4)
   auto lazy_load = [&](int64_t kb) {
     if constexpr (PH == GX_GRAD) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) le[u] = ev[GX_KB * kb + (t + 256 * u) / (TN / 4)];
+      for (int u = 0; u < TN / 32; ++u) le[u] = ev[GX_KB * kb + (t + 256 * u) / (TN / 4)];
     }
   };
   const DhA dk = dh_a_consts(bd.act);
