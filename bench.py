@@ -389,7 +389,8 @@ def main():
                 "tanh, Izmailov step sizes" + (", bf16 hidden GEMM" if args.hidden_bf16 else "") +
                 (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else "") +
                 (", sequential Net::train sweep (one branch at a time)" if args.sampler == "sequential" else ""))
-    kernel_name = {"wide": "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
+    wx_planes = path == "wide" and not args.hidden_bf16 and os.environ.get("BANN_WX_EXACT", "0") in ("", "0")
+    kernel_name = {"wide": "k_fused_grad_wx3" if wx_planes else "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
                    "layered": "k_gx_gemm"}[path]
     # ---- kernel timing for the roofline: HIP events on the library stream around
     # the timed trajectory's own gradient launches (bann_set_launch_timing); the
@@ -463,9 +464,15 @@ def main():
                                     "the masked layer with the f32 operand as three bf16 planes (3 products), the "
                                     "hidden layers with both operands as three planes (6 products), see "
                                     "bf16_pipe_frac") if path == "layered" else
+                                   ("f32-equivalent hidden-layer GEMM flops 6 n W S per branch per launch against "
+                                    "the f32 MFMA peak (the BANN_WX_EXACT=1 path's ceiling); executed on the bf16 "
+                                    "MFMA with both operands as three bf16 planes (6 products, f32-accurate), see "
+                                    "bf16_pipe_frac") if wx_planes else
                                    "hidden-layer GEMM flops 6 n W S per branch per launch",
                           **({"bf16_pipe_frac": (3 * 2 * 2 * n * m_b * widths[0] + 6 * 3 * 2 * n * widths[0] * widths[1])
-                              * nb / (grad_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF} if path == "layered" else {}),
+                              * nb / (grad_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF} if path == "layered" else
+                             {"bf16_pipe_frac": 6 * hidden_flops / (grad_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF}
+                             if wx_planes else {}),
                           "i8_mfma_tops": i8_ops / (grad_ms * 1e-3) / 1e12,
                           "mfma_busy_pmc": (mfma_pmc or {}).get("mfma_busy_per_simd_cycle"),
                           "hbm_GBps": achieved} if wide else

@@ -216,6 +216,8 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       key.L = h.L;
       key.nw = (d.nchunks + 7) / 8;
       key.full = d.nchunks == 8 * key.nw;
+    } else if (d.fused == 2) {  // wx: (act, marker chunks: the plane kernel is compiled per chunk count)
+      key.nw = d.nchunks;
     }
     LaunchGroup* grp = nullptr;
     for (auto& g : p.groups)
@@ -343,7 +345,7 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
-      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, wp, ctx->stream);
+      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, wp, ctx->stream);
     else if (g.kind == 3)
       launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, wp, ctx->stream);
     else
@@ -374,7 +376,7 @@ int run_forward(bann_ctx* ctx, const Plan& p) {
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
-      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : 0, 1, ctx->stream);
+      launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, 1, ctx->stream);
     else if (g.kind == 3)
       launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, 1, ctx->stream);
     else
@@ -761,7 +763,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   const int32_t fx_splits = best_splits(nfx, 2 * (int64_t)cus, 4);  // fx: 2 workgroups of 4 waves per CU, tiles interleaved
   int64_t nwx = 0;
   for (auto& h : ctx->br) nwx += h.dev.fused == 2;
-  const int32_t wx_splits = best_splits(nwx, 4 * (int64_t)cus, 1);  // wx: 4 two-wave workgroups per CU, a tile at a time
+  // wx: 4 two-wave workgroups per CU, a tile at a time (exact f32 MFMA); wx3: 2
+  // four-wave workgroups per CU, two tiles at a time
+  const int32_t wx_splits = wx_exact() ? best_splits(nwx, 4 * (int64_t)cus, 1) : best_splits(nwx, 2 * (int64_t)cus, 2);
   int32_t fxl_splits[9] = {};
   for (int nw = 2; nw <= 8; ++nw) {  // fxl: all waves of a workgroup on one tile; LDS- and VGPR-limited residency
     const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4), 8 / nw));

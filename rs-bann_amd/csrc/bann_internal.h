@@ -186,8 +186,10 @@ void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb,
                         float bias, double* part, double* rss_out, hipStream_t s);
 int64_t net_scratch_doubles(int64_t n);
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
-void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
-                          int write_pred, hipStream_t s);
+// mode 0 exact f32 MFMA, 1 bf16 MFMA, 2 f32-accurate bf16 planes (kernels_wx.hip)
+void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int mode,
+                          int nch, int write_pred, hipStream_t s);
+bool wx_exact();
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, hipStream_t s);
 // forward-only fx pass (predictions into st.pred, no target / backward / partials)

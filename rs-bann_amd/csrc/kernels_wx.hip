@@ -495,6 +495,467 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 2)
   if (h == 0 && lane == 0) st.rss_part[it.rss_at] = rs;
 }
 
+// ===========================================================================
+// k_fused_grad_wx3 (default wide kernel): the same six phases with the three
+// hidden GEMMs (Z1, err0, dW1) on v_mfma_f32_16x16x32_bf16 at f32 accuracy.
+// Both f32 operands are split into three bf16 planes by truncation (x = x0 + x1
+// + x2 exactly, 24 significant bits; kernels_gx.hip split3) and the six plane
+// products of weight >= 2^-16 are accumulated in f32:
+//   a b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0) + O(2^-24 |a b|),
+// so a 32-deep K step is 6 bf16 MFMAs (96 cycles) instead of 8 f32 16x16x4
+// (256 cycles).  The W1 operands are split once per item (registers); A0 and
+// delta1 are split by the wave that produces them and stored as planes.
+// A workgroup holds TWO tile pairs (4 waves; pair p takes tiles tb + p, tb + p
+// + 2, ...) so the 16 KiB W0 digit image is shared by both: 74 KiB per
+// workgroup, 2 per CU = 2 waves per SIMD as in k_fused_grad_wx.  The pairs'
+// accumulators are added in pair order at the end (one partial slab per item).
+// Plane images, per pair: A0 and delta1 as [half][plane][row][16 bf16]; row
+// 16 q + i holds individual 4 i + q; within half h of the A0 image position
+// 4 g + k holds hidden unit 16 h + 4 k + g (the order a lane of the Z0 layout
+// owns them in: one 8-byte store per plane and individual), delta1 is in
+// natural summary order.  Z1 / err0 read their B operand as one 16-byte piece
+// per plane (8 K slots), dW1 (K = individuals) both operands with
+// ds_read_b64_tr_b16 down the rows.  After its dW1 a wave's half of the A0
+// planes is dead and takes its delta0 digit image.
+// ===========================================================================
+#define WX3_PAIRS 2
+#define WX3_PLANE (64 * 32)       // bytes of one (half, plane): 64 rows x 16 bf16
+#define WX3_HALF (3 * WX3_PLANE)  // one half of a plane image (6 KiB)
+#define WX3_IMG (2 * WX3_HALF)    // one plane image (12 KiB)
+
+typedef short v4s_wx __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_wx lds_v4s_wx;
+
+namespace {
+// x = x0 + x1 + x2 by truncation (each plane the high half of an f32 word) for
+// four values: three bf16x4 planes as two dwords each
+__device__ __forceinline__ void split3x4(const float (&x)[4], v2u (&pl)[3]) {
+  uint32_t hb[4], mb[4], lb[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    hb[c] = fbits(x[c]) & 0xFFFF0000u;
+    const float r = x[c] - __builtin_bit_cast(float, hb[c]);  // exact
+    mb[c] = fbits(r) & 0xFFFF0000u;
+    lb[c] = fbits(r - __builtin_bit_cast(float, mb[c]));  // exact, <= 8 significant bits
+  }
+  // high halves of two words -> one dword (v_perm_b32: the low halves are ignored)
+  auto hh = [](uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); };
+  pl[0] = v2u{hh(hb[0], hb[1]), hh(hb[2], hb[3])};
+  pl[1] = v2u{hh(mb[0], mb[1]), hh(mb[2], mb[3])};
+  pl[2] = v2u{hh(lb[0], lb[1]), hh(lb[2], lb[3])};
+}
+__device__ __forceinline__ void split3x8(const float (&x)[8], bf16x8 (&pl)[3]) {
+  v2u a[3], b[3];
+  split3x4({x[0], x[1], x[2], x[3]}, a);
+  split3x4({x[4], x[5], x[6], x[7]}, b);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) pl[p] = __builtin_bit_cast(bf16x8, v4u{a[p].x, a[p].y, b[p].x, b[p].y});
+}
+// signed 8-bit digits of V = rint(x 2^e), |V| < 2^27, least significant first:
+// V = e3 2^24 + e2 2^16 + e1 2^8 + e0 with e0..e2 in [-128, 127] -- offsetting
+// the three low bytes by 128 makes them carry-free, flipping their top bits
+// gives the signed digits (two VALU instead of the 7-bit field extracts)
+__device__ __forceinline__ uint32_t digits8_wx(float x, int e) {
+  const int V = (int)__builtin_rintf(__builtin_amdgcn_ldexpf(x, e));
+  return ((uint32_t)V + 0x00808080u) ^ 0x00808080u;
+}
+// 2^-16 sum_d D_d 2^(8 d) from the digit sums of one tile (|D| <= 2^14): the
+// pairs D3 2^8 + D2 and D1 2^8 + D0 are exact in int32 and in f32
+__device__ __forceinline__ float comb8(v4i d) {
+  return (float)((d[3] << 8) + d[2]) + (float)((d[1] << 8) + d[0]) * 0x1p-16f;
+}
+// sum of the six plane products (small terms first), accumulated onto acc
+__device__ __forceinline__ v4f mm6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], v4f acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+// transposing read of 8 rows (two ds_read_b64_tr_b16): lane 4 uq + up of a
+// 16-lane group addresses row uq, columns 4 up .. 4 up + 3; lane li receives
+// column li of rows 0..3 (p0) and 4..7 (p1) as K slots 0..7
+__device__ __forceinline__ bf16x8 tr16x2(const char* p0, const char* p1) {
+  const v4s_wx a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_wx*)(p0));
+  const v4s_wx b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_wx*)(p1));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  return __builtin_bit_cast(bf16x8, v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]});
+}
+}  // namespace
+
+template <int ACT, int NCH>
+__global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
+    k_fused_grad_wx3(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  __shared__ __attribute__((aligned(16))) char s_w0[WX_MAXCH * WX_MB * 1024];  // W0/sigma digits, all columns
+  __shared__ __attribute__((aligned(16))) char s_img[WX3_PAIRS][2][WX3_IMG];  // per pair: A0 planes, delta1 planes
+  __shared__ __attribute__((aligned(16))) char s_x[WX3_PAIRS][2][WX_SLOT];    // tile images (double-buffered)
+  __shared__ __attribute__((aligned(16))) float s_y[WX3_PAIRS][2][64];
+  __shared__ __attribute__((aligned(16))) float s_po[WX3_PAIRS][2][64];
+
+  const GradItem it = items[blockIdx.x];
+  const int b = it.branch;
+  const BranchDev& bd = st.br[b];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = wv & 1, pr = wv >> 1;  // this wave's half and tile pair
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15;
+  constexpr int nch = NCH;  // marker chunks of 64 (bd.nchunks, checked at launch)
+  const int m = bd.m, w0 = bd.widths[0], S = bd.widths[1];
+  const int64_t n = st.n;
+  const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
+  const float* th = st.theta + bd.p_off;
+
+  for (int t = threadIdx.x; t < nch * WX_MB * 64; t += 64 * 2 * WX3_PAIRS)
+    *reinterpret_cast<v4i*>(&s_w0[t * 16]) = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + (int64_t)t * 16);
+
+  float zs[4], c0v[4], b1v[4], w2v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * (4 * h + k) + g;
+    zs[k] = c < w0 ? st.fc[b].scale[c] : 0.f;
+    c0v[k] = c < w0 ? st.fc[b].c0[c] : 0.f;
+    const int s = 16 * h + 4 * g + k;
+    b1v[k] = s < S ? th[bd.boff[1] + s] : 0.f;
+    w2v[k] = s < S ? th[bd.woff[2] + s] : 0.f;
+  }
+  auto W1at = [&](int c, int s) { return (c < w0 && s < S) ? th[bd.woff[1] + s * w0 + c] : 0.f; };
+  // W1 planes.  Z1 (A = W1^T rows of own summary units 16 h + i): K slot 8 g + j
+  // is A0 image position p = 8 g + j, hidden unit 16 (p >> 4) + 4 (p & 3) + ((p >> 2) & 3).
+  // err0 (A rows permuted so the result lands in the Z0 layout): row i = hidden
+  // unit 16 h + 4 (i & 3) + (i >> 2), K slot 8 g + j = summary unit 8 g + j.
+  bf16x8 wz[3], we3[3];
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int p = 8 * g + j;
+      v[j] = W1at(16 * (p >> 4) + 4 * (p & 3) + ((p >> 2) & 3), 16 * h + i);
+    }
+    split3x8(v, wz);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = W1at(16 * h + 4 * (i & 3) + (i >> 2), 8 * g + j);
+    split3x8(v, we3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int tq = i >> 1, tp = lane & 1, gsw = g & 1;
+  const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
+  const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
+  const int pe = i, po = (i + 8) & 15;
+  const uint32_t boe = (uint32_t)(pe * 16 + 4 * (2 * ((g >> 1) ^ (pe >> 3)) + (g & 1)));
+  const uint32_t boo = (uint32_t)(po * 16 + 4 * (2 * ((g >> 1) ^ (po >> 3)) + (g & 1)));
+  const int iota = 4 * i + g;
+  char* const sA = s_img[pr][0];
+  char* const sD = s_img[pr][1];
+  const uint32_t wr_off = (uint32_t)(h * WX3_HALF + i * 32 + 8 * g);          // + 512 q: own half, row 16 q + i
+  const uint32_t rd_off = (uint32_t)((g >> 1) * WX3_HALF + i * 32 + 16 * (g & 1));  // + 512 q: K slots 8 g ..
+  const uint32_t tr_off = (uint32_t)((8 * g + (i >> 2)) * 32 + 8 * (i & 3));  // + 1024 ks: rows 32 ks + 8 g ..
+  char* const sdig = sA + h * WX3_HALF;  // delta0 digits: the own (dead) half of the A0 planes
+  char* const sd_w = sdig + (i >> 2) * 256 + (4 * g + (i & 3)) * 16;
+  const char* const sd_r = sdig + g * 256 + tq * 16 + 8 * tp;
+  const float* ybr = st.y + bd.y_off;
+  float* predb = st.pred + bd.y_off;
+  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
+  const int64_t tile_bytes = (int64_t)nch * 1024;
+  auto issue_tile = [&](int tt, int sl) {
+    if (h < nch) glds16(xsrc + (int64_t)tt * tile_bytes + h * 1024, &s_x[pr][sl][h * 1024]);
+    if (h == 0) {
+      const int64_t row = 64 * (int64_t)tt + iota;
+      glds4(ybr + (row < n ? row : n - 1), &s_y[pr][sl][0]);
+    }
+  };
+
+  float dW0a[4 * WX_MAXCH][4];
+#pragma unroll
+  for (int u = 0; u < 4 * WX_MAXCH; ++u)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dW0a[u][k] = 0.f;
+  float db0a[4], db1a[4], dW2a[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) db0a[k] = db1a[k] = dW2a[k] = 0.f;
+  v4f dW1a[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+  double rss = 0.0;
+
+  // rounds of WX3_PAIRS tiles; a pair without a tile in the last round runs on
+  // its stale slot with every row invalid (e = 0: it adds exactly nothing)
+  const int nrounds = (te - tb + WX3_PAIRS - 1) / WX3_PAIRS;
+  int sl = 0;
+  if (tb + pr < te) issue_tile(tb + pr, 0);
+  for (int rd = 0; rd < nrounds; ++rd, sl ^= 1) {
+    const int tt = tb + WX3_PAIRS * rd + pr;
+    const bool live = tt < te;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tt + WX3_PAIRS < te) issue_tile(tt + WX3_PAIRS, sl ^ 1);
+    const char* xs = &s_x[pr][sl][0];
+
+    // ---- 1. masked layer forward (as k_fused_grad_wx) ----
+    float z0[4][4], a0[4][4];
+    {
+      v4i fa[4][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fa[k][q] = v4i{0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < WX_MAXCH; ++c) {
+        if (c < nch) {
+          const v4u X = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+          const v4i B0 = (v4i)(X & 0x03030303u);
+          const v4i B1 = (v4i)(X & 0x0C0C0C0Cu);
+          const v4i B2 = (v4i)(X & 0x30303030u);
+          const v4i B3 = (v4i)((X >> 2u) & 0x30303030u);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const v4i A = *reinterpret_cast<const v4i*>(&s_w0[((c * WX_MB + 4 * h + k) * 64 + lane) * 16]);
+            fa[k][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B0, fa[k][0], 0, 0, 0);
+            fa[k][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B1, fa[k][1], 0, 0, 0);
+            fa[k][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B2, fa[k][2], 0, 0, 0);
+            fa[k][3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B3, fa[k][3], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z0[k][0] = (0x1p-7f * zs[k]) * comb4p(fa[k][0]) + c0v[k];
+        z0[k][1] = (0x1p-9f * zs[k]) * comb4p(fa[k][1]) + c0v[k];
+        z0[k][2] = (0x1p-11f * zs[k]) * comb4p(fa[k][2]) + c0v[k];
+        z0[k][3] = (0x1p-11f * zs[k]) * comb4p(fa[k][3]) + c0v[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a0[k][q] = act_h_t<ACT>(z0[k][q]);
+      }
+    }
+    // A0 planes: own half, individual 4 i + q, positions 4 g .. 4 g + 3 (hidden 16 h + 4 k + g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v2u pl[3];
+      split3x4({a0[0][q], a0[1][q], a0[2][q], a0[3][q]}, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<v2u*>(sA + wr_off + p * WX3_PLANE + 512 * q) = pl[p];
+    }
+    LDS_BARRIER();  // the full A0 planes of the pair
+
+    // ---- 2. Z1^T = W1^T A0^T, own summary units (K = the 32 hidden units) ----
+    v4f z1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bf16x8 bq[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(sA + rd_off + p * WX3_PLANE + 512 * q);
+      z1[q] = mm6(wz, bq, v4f{0.f, 0.f, 0.f, 0.f});
+    }
+
+    // ---- 3. head (as k_fused_grad_wx) ----
+    float a1[4][4], pp[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pp[q] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        z1[q][r] += b1v[r];
+        a1[q][r] = act_h_t<ACT>(z1[q][r]);
+        pp[q] = fmaf(a1[q][r], w2v[r], pp[q]);
+      }
+    }
+    xpose4f(pp[0], pp[1], pp[2], pp[3]);
+    s_po[pr][h][lane] = (pp[0] + pp[1]) + (pp[2] + pp[3]);
+    LDS_BARRIER();  // both halves' partial outputs
+    const float out = s_po[pr][0][lane] + s_po[pr][1][lane];
+    const int64_t row = 64 * (int64_t)tt + iota;
+    const bool valid = live && row < n;
+    const float yv = s_y[pr][sl][lane];
+    const float e = valid ? out - yv : 0.f;
+    if (h == 0 && write_pred && valid) predb[row] = out;
+    rss += (double)e * (double)e;
+    float eq[4] = {e, e, e, e};
+    xpose4f(eq[0], eq[1], eq[2], eq[3]);
+    float d1[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float sw = 0.f, sd = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        d1[q][r] = act_dh_t<ACT>(z1[q][r], a1[q][r]) * (eq[q] * w2v[r]);
+        sw = fmaf(a1[q][r], eq[q], sw);
+        sd += d1[q][r];
+      }
+      dW2a[r] += sw;
+      db1a[r] += sd;
+    }
+    // delta1 planes: own half, individual 4 i + q, summary units 16 h + 4 g .. + 3
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v2u pl[3];
+      split3x4({d1[q][0], d1[q][1], d1[q][2], d1[q][3]}, pl);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<v2u*>(sD + wr_off + p * WX3_PLANE + 512 * q) = pl[p];
+    }
+    LDS_BARRIER();  // the full delta1 planes of the pair
+
+    // ---- 4. err0 = delta1 W1^T, own hidden units in the Z0 layout; delta0 ----
+    float d0[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bf16x8 bq[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(sD + rd_off + p * WX3_PLANE + 512 * q);
+      const v4f acc = mm6(we3, bq, v4f{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d0[k][q] = act_dh_t<ACT>(z0[k][q], a0[k][q]) * acc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) db0a[k] += (d0[k][0] + d0[k][1]) + (d0[k][2] + d0[k][3]);
+
+    // ---- 5. dW1 = A0^T delta1 (rows: own hidden units in position order, K = individuals) ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ta[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const char* a = sA + h * WX3_HALF + p * WX3_PLANE + 1024 * ks + tr_off;
+        ta[p] = tr16x2(a, a + 128);
+      }
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        bf16x8 tdl[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const char* d = sD + sb * WX3_HALF + p * WX3_PLANE + 1024 * ks + tr_off;
+          tdl[p] = tr16x2(d, d + 128);
+        }
+        dW1a[sb] = mm6(ta, tdl, dW1a[sb]);
+      }
+    }
+
+    // ---- 6. delta0 digits over the own dead A0 half, masked backward (as k_fused_grad_wx) ----
+    float sc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t mx = row_max_u(max(max(fbits(d0[k][0]) & 0x7FFFFFFFu, fbits(d0[k][1]) & 0x7FFFFFFFu),
+                                        max(fbits(d0[k][2]) & 0x7FFFFFFFu, fbits(d0[k][3]) & 0x7FFFFFFFu)));
+      const int R = (int)((mx >> 23) & 0xFFu) + 2;
+      sc[k] = __builtin_amdgcn_ldexpf(1.f, R - 137);  // comb8 carries 2^-16
+      uint32_t dq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dq[q] = digits8_wx(d0[k][q], 153 - R);
+      xpose4(dq[0], dq[1], dq[2], dq[3]);
+      *reinterpret_cast<v4u*>(sd_w + k * 1024) = v4u{dq[0], dq[1], dq[2], dq[3]};
+    }
+    v4i Ab[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ab[k] = lds_tr8_pair(sd_r + k * 1024, sd_r + k * 1024 + 8 * 16);
+#pragma unroll
+    for (int u = 0; u < 4 * WX_MAXCH; ++u) {
+      if (u < 4 * nch) {
+        const uint32_t wvv = *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe));
+        const v4i Bv = v4i{(int)(wvv & 0x03030303u), (int)((wvv >> 2) & 0x03030303u),
+                           (int)((wvv >> 4) & 0x03030303u), (int)((wvv >> 6) & 0x03030303u)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const v4i t = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ab[k], Bv, v4i{0, 0, 0, 0}, 0, 0, 0);
+          dW0a[u][k] = fmaf(comb8(t), sc[k], dW0a[u][k]);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is past its last tile: the plane images are free
+
+  // ---- the two pairs' accumulators, added in pair order ----
+  constexpr int NV = 4 * 4 * WX_MAXCH + 4 + 4 + 4 + 8;
+  float* red = reinterpret_cast<float*>(&s_img[0][0][0]);
+  double* redd = reinterpret_cast<double*>(red + 2 * NV * 64);
+  {
+    float* o = red + h * NV * 64 + lane;
+    if (pr == 1) {
+      int v = 0;
+#pragma unroll
+      for (int u = 0; u < 4 * WX_MAXCH; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[64 * v++] = dW0a[u][k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        o[64 * v++] = db0a[k];
+        o[64 * v++] = db1a[k];
+        o[64 * v++] = dW2a[k];
+      }
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[64 * v++] = dW1a[sb][r];
+      redd[h * 64 + lane] = rss;
+    }
+    __syncthreads();
+    if (pr == 1) return;
+    int v = 0;
+#pragma unroll
+    for (int u = 0; u < 4 * WX_MAXCH; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dW0a[u][k] += o[64 * v++];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      db0a[k] += o[64 * v++];
+      db1a[k] += o[64 * v++];
+      dW2a[k] += o[64 * v++];
+    }
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dW1a[sb][r] += o[64 * v++];
+    rss += redd[h * 64 + lane];
+  }
+
+  // ---- epilogue: this half's part of the item's partial slab ----
+  float* part = st.part + it.part_at;
+  float db0[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) db0[k] = row_sum(db0a[k]);
+#pragma unroll
+  for (int u = 0; u < 4 * WX_MAXCH; ++u) {
+    const int j = 16 * u + i;
+    if (u < 4 * nch && j < m) {
+      const float mu = st.mu[bd.mk_off + j], sg = st.sigma[bd.mk_off + j];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * (4 * h + k) + g;
+        if (c < w0) part[bd.woff[0] + c * m + j] = sg > 0.f ? (dW0a[u][k] - mu * db0[k]) / sg : 0.f;
+      }
+    }
+  }
+  if (i == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * (4 * h + k) + g < w0) part[bd.boff[0] + 4 * (4 * h + k) + g] = db0[k];
+  }
+  // dW1 lane (n = i, g): rows 4 g + r = A0 positions 16 h + 4 g + r = hidden 16 h + 4 r + g
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 16 * h + 4 * r + g, s = 16 * sb + i;
+      if (c < w0 && s < S) part[bd.woff[1] + s * w0 + c] = dW1a[sb][r];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int s = 16 * h + 4 * g + r;
+    const float v1 = row_sum(db1a[r]), v2 = row_sum(dW2a[r]);
+    if (i == 0 && s < S) {
+      part[bd.boff[1] + s] = v1;
+      part[bd.woff[2] + s] = v2;
+    }
+  }
+  const double rs = wave_sum_d(rss);
+  if (h == 0 && lane == 0) st.rss_part[it.rss_at] = rs;
+}
+
+bool wx_exact() {
+  const char* ex = getenv("BANN_WX_EXACT");  // 1: the hidden GEMMs on the exact-f32 MFMA (k_fused_grad_wx)
+  return ex && atoi(ex) != 0;
+}
+
 template <int BF>
 static void launch_wx_bf(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * WX_WAVES);
@@ -507,9 +968,29 @@ static void launch_wx_bf(const DevState& st, const GradItem* items, int32_t nite
   }
 }
 
-void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int bf16,
-                          int write_pred, hipStream_t s) {
+template <int NCH>
+static void launch_wx3(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * 2 * WX3_PAIRS);
+  switch (act) {
+    case 0: hipLaunchKernelGGL((k_fused_grad_wx3<0, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_wx3<1, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_wx3<2, NCH>), grid, block, 0, s, st, items, wp); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_wx3<3, NCH>), grid, block, 0, s, st, items, wp); break;
+    default: hipLaunchKernelGGL((k_fused_grad_wx3<4, NCH>), grid, block, 0, s, st, items, wp); break;
+  }
+}
+
+// mode: 0 = exact f32 MFMA hidden GEMMs (k_fused_grad_wx, BANN_WX_EXACT=1), 1 =
+// bf16 MFMA (opt-in, reduced precision), 2 = f32-accurate bf16 planes (default)
+void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int mode,
+                          int nch, int write_pred, hipStream_t s) {
   if (nitems <= 0) return;
-  if (bf16) launch_wx_bf<1>(st, items, nitems, act, write_pred, s);
-  else launch_wx_bf<0>(st, items, nitems, act, write_pred, s);
+  if (mode == 1) {
+    launch_wx_bf<1>(st, items, nitems, act, write_pred, s);
+  } else if (mode == 0) {
+    launch_wx_bf<0>(st, items, nitems, act, write_pred, s);
+  } else {
+    if (nch == 1) launch_wx3<1>(st, items, nitems, act, write_pred, s);
+    else launch_wx3<2>(st, items, nitems, act, write_pred, s);
+  }
 }

@@ -733,6 +733,30 @@ def test_wide_packed_deterministic(Ctx):
     ctx.close()
 
 
+def test_wide_exact_f32_path(Ctx):
+    """BANN_WX_EXACT=1 keeps the hidden GEMMs on the exact f32 MFMA
+    (k_fused_grad_wx, one tile per two-wave workgroup); the default plane path
+    (k_fused_grad_wx3: three bf16 planes per f32 operand, six products) and it
+    both match the oracle to 1e-5 and each other to f32 rounding."""
+    ctx, specs = _wide_problem(Ctx, 45, nb=2, widths=(32, 27, 1))
+    g_planes = [ctx.log_density_gradient(b) for b in range(2)]
+    ctx.close()
+    os.environ["BANN_WX_EXACT"] = "1"
+    try:
+        ctx, _ = _wide_problem(Ctx, 45, nb=2, widths=(32, 27, 1))
+        g_exact = [ctx.log_density_gradient(b) for b in range(2)]
+        ctx.close()
+    finally:
+        del os.environ["BANN_WX_EXACT"]
+    for b, s in enumerate(specs):
+        ogw, ogb, orss = O.log_density_gradient(s["branch"], s["X"], s["y"])
+        ref = O.param_vec(ogw, ogb)
+        for grad, rss in (g_planes[b], g_exact[b]):
+            assert norm_rel(grad, ref) < TOL, b
+            assert scalar_close(rss, orss)
+        assert norm_rel(g_planes[b][0], g_exact[b][0]) < 2e-6
+
+
 def test_wide_bf16_hidden_gemm(Ctx):
     """bann_set_hidden_gemm_bf16 (C5's bf16 hidden GEMM): the hidden-layer GEMMs
     round their operands to bf16 (8-bit mantissa), so the gradient agrees with
