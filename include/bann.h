@@ -363,8 +363,10 @@ int bann_branch_kernel_path(const bann_ctx* ctx, int32_t b);
 /* name of the fused gradient kernel family used for branches of <= 512 markers */
 const char* bann_fused_kernel_name(void);
 /* wide kernel: run the hidden-layer GEMMs (forward, error propagation, dW1) on
- * bf16 MFMA (1) instead of exact f32 MFMA (0, default).  BASELINE config C5's
- * "bf16 hidden GEMM on MFMA vs fp32": 16x the matrix rate, bf16 operand
+ * the bf16 MFMA with bf16-rounded operands (1) instead of at f32 accuracy (0,
+ * default: each f32 operand as three bf16 planes, six plane products per
+ * product on the bf16 MFMA; BANN_WX_EXACT=1 selects the f32 MFMA instead).
+ * BASELINE config C5's "bf16 hidden GEMM on MFMA vs fp32": bf16 operand
  * rounding (~1e-3 relative on gradients; not parity-exact).  Any time. */
 int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled);
 /* force every branch onto the layered gx path (0) or allow the fused kernels (1) */

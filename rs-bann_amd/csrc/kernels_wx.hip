@@ -513,10 +513,11 @@ __global__ void __launch_bounds__(64 * WX_WAVES, 2)
 // 16 q + i holds individual 4 i + q; within half h of the A0 image position
 // 4 g + k holds hidden unit 16 h + 4 k + g (the order a lane of the Z0 layout
 // owns them in: one 8-byte store per plane and individual), delta1 is in
-// natural summary order.  Z1 / err0 read their B operand as one 16-byte piece
-// per plane (8 K slots), dW1 (K = individuals) both operands with
-// ds_read_b64_tr_b16 down the rows.  After its dW1 a wave's half of the A0
-// planes is dead and takes its delta0 digit image.
+// natural summary order; the four 8-byte pieces of a 32-byte half-row are
+// swizzled by row (bank-conflict-free stores and reads).  Z1 / err0 read their B
+// operand as two pieces per plane (8 K slots), dW1 (K = individuals) both
+// operands with ds_read_b64_tr_b16 down the rows.  After its dW1 a wave's half
+// of the A0 planes is dead and takes its delta0 digit image.
 // ===========================================================================
 #define WX3_PAIRS 2
 #define WX3_PLANE (64 * 32)       // bytes of one (half, plane): 64 rows x 16 bf16
@@ -582,6 +583,12 @@ __device__ __forceinline__ bf16x8 tr16x2(const char* p0, const char* p1) {
   const v4s_wx b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_wx*)(p1));
   typedef short v8s __attribute__((ext_vector_type(8)));
   return __builtin_bit_cast(bf16x8, v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]});
+}
+// two 8-byte pieces (ds_read_b64 each) as one 8-deep bf16 fragment
+__device__ __forceinline__ bf16x8 rd_pieces(const char* base, uint32_t o0, uint32_t o1) {
+  const v2u a = *reinterpret_cast<const v2u*>(base + o0);
+  const v2u c = *reinterpret_cast<const v2u*>(base + o1);
+  return __builtin_bit_cast(bf16x8, v4u{a.x, a.y, c.x, c.y});
 }
 }  // namespace
 
@@ -650,9 +657,19 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
   const int iota = 4 * i + g;
   char* const sA = s_img[pr][0];
   char* const sD = s_img[pr][1];
-  const uint32_t wr_off = (uint32_t)(h * WX3_HALF + i * 32 + 8 * g);          // + 512 q: own half, row 16 q + i
-  const uint32_t rd_off = (uint32_t)((g >> 1) * WX3_HALF + i * 32 + 16 * (g & 1));  // + 512 q: K slots 8 g ..
-  const uint32_t tr_off = (uint32_t)((8 * g + (i >> 2)) * 32 + 8 * (i & 3));  // + 1024 ks: rows 32 ks + 8 g ..
+  // 8-byte piece P of plane row rho sits at position P ^ swz((rho >> 2) & 3) of its
+  // 32-byte half-row (swz swaps the two bits): the stores (16 lanes = 16 rows, one
+  // piece each, banks mod 32) and the Z1 / err0 reads (32 lanes, mod 64) are then
+  // conflict-free (row-major without it: 4-way on the stores)
+  auto swz = [](int v) { return ((v & 1) << 1) | (v >> 1); };
+  const int sw_i = swz((i >> 2) & 3);
+  const uint32_t wr_off = (uint32_t)(h * WX3_HALF + i * 32 + 8 * (g ^ sw_i));  // + 512 q: own half, row 16 q + i
+  const uint32_t rd_off0 = (uint32_t)((g >> 1) * WX3_HALF + i * 32 + 8 * ((2 * (g & 1)) ^ sw_i));  // K slots 8 g .. + 3
+  const uint32_t rd_off1 = (uint32_t)((g >> 1) * WX3_HALF + i * 32 + 8 * ((2 * (g & 1) + 1) ^ sw_i));  // 8 g + 4 ..
+  // dW1 (K = individuals): K slots 8 g + j of block ks are rows 32 ks + 16 (j >> 2) + 4 g
+  // + (j & 3) -- the two 16-lane groups of a 32-lane bank group read rows 0-3 / 4-7
+  // of an 8-row bank window (conflict-free); + 512 for j >= 4, + 1024 ks
+  const uint32_t tr_off = (uint32_t)((4 * g + (i >> 2)) * 32 + 8 * ((i & 3) ^ swz(g)));
   char* const sdig = sA + h * WX3_HALF;  // delta0 digits: the own (dead) half of the A0 planes
   char* const sd_w = sdig + (i >> 2) * 256 + (4 * g + (i & 3)) * 16;
   const char* const sd_r = sdig + g * 256 + tq * 16 + 8 * tp;
@@ -744,7 +761,7 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
     for (int q = 0; q < 4; ++q) {
       bf16x8 bq[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(sA + rd_off + p * WX3_PLANE + 512 * q);
+      for (int p = 0; p < 3; ++p) bq[p] = rd_pieces(sA + p * WX3_PLANE + 512 * q, rd_off0, rd_off1);
       z1[q] = mm6(wz, bq, v4f{0.f, 0.f, 0.f, 0.f});
     }
 
@@ -801,7 +818,7 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
     for (int q = 0; q < 4; ++q) {
       bf16x8 bq[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bq[p] = *reinterpret_cast<const bf16x8*>(sD + rd_off + p * WX3_PLANE + 512 * q);
+      for (int p = 0; p < 3; ++p) bq[p] = rd_pieces(sD + p * WX3_PLANE + 512 * q, rd_off0, rd_off1);
       const v4f acc = mm6(we3, bq, v4f{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int k = 0; k < 4; ++k) d0[k][q] = act_dh_t<ACT>(z0[k][q], a0[k][q]) * acc[k];
@@ -816,7 +833,7 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const char* a = sA + h * WX3_HALF + p * WX3_PLANE + 1024 * ks + tr_off;
-        ta[p] = tr16x2(a, a + 128);
+        ta[p] = tr16x2(a, a + 512);
       }
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb) {
@@ -824,7 +841,7 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           const char* d = sD + sb * WX3_HALF + p * WX3_PLANE + 1024 * ks + tr_off;
-          tdl[p] = tr16x2(d, d + 128);
+          tdl[p] = tr16x2(d, d + 512);
         }
         dW1a[sb] = mm6(ta, tdl, dW1a[sb]);
       }
