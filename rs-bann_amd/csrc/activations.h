@@ -63,6 +63,17 @@ __device__ __forceinline__ float tanh5(float x) {
   return fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 
+// tanh and its derivative without cancellation: with r = 1 / (e^{2|x|} + 1) <= 1/2,
+// tanh x = sign(x) (1 - 2 r) and 1 - tanh^2 x = 4 r (1 - r), where 1 - r >= 1/2:
+// accurate relative to the derivative itself where tanh saturates (1 - h^2 from the
+// rounded h loses it there: |h| = 1 - 1e-3 leaves ~3e-5 relative error)
+__device__ __forceinline__ float tanh_r(float x, float& r) {
+  const float e = __builtin_amdgcn_exp2f(fabsf(x) * 2.8853900817779268f);  // 2 log2(e); inf -> r = 0
+  r = __builtin_amdgcn_rcpf(e + 1.f);
+  return copysignf(fmaf(-2.f, r, 1.f), x);
+}
+__device__ __forceinline__ float dtanh_r(float r) { return (4.f * r) * (1.f - r); }
+
 // compile-time activation (fused kernel): h and dh/dx without branches on the code
 template <int ACT>
 __device__ __forceinline__ float act_h_t(float x) {

@@ -586,7 +586,7 @@ __global__ void __launch_bounds__(256, GX_NBUF == 1 ? (PH == GX_GRAD ? 3 : 4) : 
 // stays selectable (BANN_GX_EXACT=1: exact f32 products).
 // LDS images [row][k] with 72-element rows (conflict-free 16-byte fragment reads).
 // ---------------------------------------------------------------------------
-#define GX_LDH 72  // bf16 row stride (elements)
+#define GX_LDH 80  // bf16 row stride (elements): 40 dwords, conflict-free row and transposing reads (below)
 #ifndef GX_F64_EVERY
 #define GX_F64_EVERY 4  // 64-deep K blocks per f32 accumulation before the f64 sum (256 rows / markers)
 #endif
@@ -624,8 +624,16 @@ __device__ __forceinline__ bf16x8 tr16_pair(const __bf16* p0, const __bf16* p1) 
 }
 }  // namespace
 
+// K slot of logical k (0..63) of a 64-deep K block in the b3 stages: the K slots
+// 8 lq + j of half ks are k = 32 ks + 16 (j >> 2) + 4 lq + (j & 3), so the two
+// 16-lane groups of a transposing read (rows 4 lq + tq) take rows 0-3 / 4-7 of an
+// 8-row bank window; operands read along their rows store logical K group c (4
+// consecutive k) at this element offset
+__device__ __forceinline__ int b3_kpos(int c) { return 32 * (c >> 3) + 8 * (c & 3) + 4 * ((c >> 2) & 1); }
+
 // LDS: the genotype chunk as G[marker][individual] (16 consecutive individuals per
-// thread: two 16-byte stores); FWD0 takes its A fragments (rows = individuals,
+// thread: two 16-byte stores; GRAD0, whose K is the individuals, four 8-byte stores
+// at b3_kpos); FWD0 takes its A fragments (rows = individuals,
 // K = markers) from it by transposing reads and its B fragments from the W0 planes
 // [column][marker] (pre-split by k_gx_prep); GRAD0 takes A (rows = markers, K =
 // individuals) by row reads and B from the delta0 planes [individual][column]
@@ -703,14 +711,22 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
         v0[s2] = (__bf16)(float)((rg >> (2 * s2)) & 3u);
         v1[s2] = (__bf16)(float)((rg >> (2 * s2 + 16)) & 3u);
       }
-      *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq] = v0;
-      *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq + 8] = v1;
+      if constexpr (PH == GX_FWD0) {
+        *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq] = v0;
+        *(bf16x8*)&Gs[jl * GX_LDH + 16 * dq + 8] = v1;
+      } else {
+        *(bf16x4*)&Gs[jl * GX_LDH + b3_kpos(4 * dq)] = bf16x4{v0[0], v0[1], v0[2], v0[3]};
+        *(bf16x4*)&Gs[jl * GX_LDH + b3_kpos(4 * dq + 1)] = bf16x4{v0[4], v0[5], v0[6], v0[7]};
+        *(bf16x4*)&Gs[jl * GX_LDH + b3_kpos(4 * dq + 2)] = bf16x4{v1[0], v1[1], v1[2], v1[3]};
+        *(bf16x4*)&Gs[jl * GX_LDH + b3_kpos(4 * dq + 3)] = bf16x4{v1[4], v1[5], v1[6], v1[7]};
+      }
     }
     if constexpr (PH == GX_FWD0) {
 #pragma unroll
       for (int u = 0; u < 6; ++u) {
         const int e = t + 256 * u, pl = e >> 9, row = (e >> 3) & 63, pc = e & 7;
-        *(v4i*)&Bs[pl][row * GX_LDH + 8 * pc] = rw[u];
+        *(v2i*)&Bs[pl][row * GX_LDH + b3_kpos(2 * pc)] = v2i{rw[u][0], rw[u][1]};
+        *(v2i*)&Bs[pl][row * GX_LDH + b3_kpos(2 * pc + 1)] = v2i{rw[u][2], rw[u][3]};
       }
     } else {
       blk_fix(rb, BlkBounds{64 * (int64_t)kb, rows, 64 * tn, wo});
@@ -750,11 +766,12 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
     if (kb + 1 < kb1) load(kb + 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int ko = 32 * ks + 8 * lq;  // this lane group's 8 K slots
+      const int ko = 32 * ks + 8 * lq;          // this lane group's 8 K slots (row reads)
+      const int kr = 32 * ks + 4 * lq + tq;     // their rows 0-3 (+ 16: 4-7) in transposing reads
       bf16x8 a0, a1;
       if constexpr (PH == GX_FWD0) {  // rows = individuals, K = markers: transposed from Gs
-        a0 = tr16_pair(&Gs[(ko + tq) * GX_LDH + ar + 4 * tp], &Gs[(ko + 4 + tq) * GX_LDH + ar + 4 * tp]);
-        a1 = tr16_pair(&Gs[(ko + tq) * GX_LDH + ar + 16 + 4 * tp], &Gs[(ko + 4 + tq) * GX_LDH + ar + 16 + 4 * tp]);
+        a0 = tr16_pair(&Gs[kr * GX_LDH + ar + 4 * tp], &Gs[(kr + 16) * GX_LDH + ar + 4 * tp]);
+        a1 = tr16_pair(&Gs[kr * GX_LDH + ar + 16 + 4 * tp], &Gs[(kr + 16) * GX_LDH + ar + 16 + 4 * tp]);
       } else {  // rows = markers, K = individuals: row reads
         a0 = *(const bf16x8*)&Gs[(ar + li) * GX_LDH + ko];
         a1 = *(const bf16x8*)&Gs[(ar + 16 + li) * GX_LDH + ko];
@@ -766,9 +783,8 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
           b0 = *(const bf16x8*)&Bs[pl][(bc + li) * GX_LDH + ko];
           b1 = *(const bf16x8*)&Bs[pl][(bc + 16 + li) * GX_LDH + ko];
         } else {  // B[k = individual][n = column] transposed from Bs[individual][column]
-          b0 = tr16_pair(&Bs[pl][(ko + tq) * GX_LDH + bc + 4 * tp], &Bs[pl][(ko + 4 + tq) * GX_LDH + bc + 4 * tp]);
-          b1 = tr16_pair(&Bs[pl][(ko + tq) * GX_LDH + bc + 16 + 4 * tp],
-                         &Bs[pl][(ko + 4 + tq) * GX_LDH + bc + 16 + 4 * tp]);
+          b0 = tr16_pair(&Bs[pl][kr * GX_LDH + bc + 4 * tp], &Bs[pl][(kr + 16) * GX_LDH + bc + 4 * tp]);
+          b1 = tr16_pair(&Bs[pl][kr * GX_LDH + bc + 16 + 4 * tp], &Bs[pl][(kr + 16) * GX_LDH + bc + 16 + 4 * tp]);
         }
         acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[0], 0, 0, 0);
         acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[1], 0, 0, 0);
@@ -854,17 +870,32 @@ __global__ void __launch_bounds__(256, PH == GX_GRAD0 ? 3 : 4)
 // rows).  BANN_GX_EXACT=1 keeps k_gx_gemm (f32 MFMA) for every phase.
 // ---------------------------------------------------------------------------
 #define GX_KB 32  // K block depth
-#define GX_RK 40  // [row][k] stride (bf16 elements): 80-byte rows, conflict-free 16-byte reads
+#define GX_RK 40  // [row][k] stride (bf16 elements): 80-byte rows
 
 namespace {
 // LDS geometry of a staged operand block of R (MFMA) rows x 32 K as three bf16 planes:
-// [row][k] rows of GX_RK, or [k][row] rows of KRS = R + 8 (+ 64 at R = 128: a
-// row stride of 36 dwords mod 64 keeps the ds_read_b64_tr_b16 pairs conflict-free)
+// [row][k] rows of GX_RK, or [k][row] rows of KRS = R + 16.  Bank conflicts
+// (MI355X_MICROARCH.md LDS table; PMC: SQ_LDS_BANK_CONFLICT was 20-45 % of the
+// phases' LDS cycles before this layout):
+//  - [row][k]: the 16-byte K chunk q of row r sits at chunk q ^ rk_sw(r), which
+//    makes the fragment reads (ds_read_b128, lane groups {0-3,12-15,20-27}, ...)
+//    conflict-free at the 80-byte stride;
+//  - [k][row]: the K slots 8 lq + j of a fragment are rows 16 (j >> 2) + 4 lq +
+//    (j & 3) (kr_row), so the two 16-lane groups of a transposing read take rows
+//    0-3 / 4-7 of an 8-row window (conflict-free at R + 16); a [row][k] operand
+//    paired with a [k][row] one (BWD's A) stores logical k at that K slot (PERM).
 template <int R, bool RK>
 struct Geo {
-  static constexpr int KRS = R == 64 ? 72 : 200;
+  static constexpr int KRS = R + 16;
   static constexpr int PL = RK ? R * GX_RK : GX_KB * KRS;  // elements per plane
 };
+__device__ __forceinline__ int rk_sw(int r) { return ((r >> 2) ^ (r >> 3)) & 1; }
+// element offset of logical K group c (4 consecutive k) of [row][k] row r
+template <bool PERM>
+__device__ __forceinline__ int rk_off(int r, int c) {
+  const int p = PERM ? 8 * (c & 3) + 4 * (c >> 2) : 4 * c;  // K slot of logical k = 4 c
+  return r * GX_RK + 8 * ((p >> 3) ^ rk_sw(r)) + (p & 7);
+}
 // an R (MFMA rows) x 32 (K) block of an f32 matrix, R / 32 x 4 consecutive elements
 // per thread.  RK: M[r][k], thread e = t + 256 u holds row e >> 3, k 4 (e & 7) .. +3.
 // KR: M[k][r], thread e holds k e / (R / 4), rows 4 (e % (R / 4)) .. +3.  Elements
@@ -901,7 +932,7 @@ __device__ __forceinline__ void blk2_load(Blk2<R>& s, const float* __restrict__ 
 }
 // mask, split into the three planes P[3][PL] and store; csp (KR only) += the
 // masked values per row of the thread's four
-template <bool RK, bool CS, int R>
+template <bool RK, bool CS, int R, bool PERM = false>
 __device__ __forceinline__ void blk2_store(Blk2<R>& s, const Blk2Bounds& k, __bf16* P, double (&csp)[4]) {
   constexpr int PL = Geo<R, RK>::PL, KRS = Geo<R, RK>::KRS;
 #pragma unroll
@@ -923,7 +954,7 @@ __device__ __forceinline__ void blk2_store(Blk2<R>& s, const Blk2Bounds& k, __bf
       l4[c] = ll;
       if constexpr (CS) csp[c] += (double)x[c];
     }
-    const int off = RK ? (e >> 3) * GX_RK + 4 * (e & 7) : (e / (R / 4)) * KRS + 4 * (e % (R / 4));
+    const int off = RK ? rk_off<PERM>(e >> 3, e & 7) : (e / (R / 4)) * KRS + 4 * (e % (R / 4));
     *(bf16x4*)&P[off] = h4;
     *(bf16x4*)&P[PL + off] = m4;
     *(bf16x4*)&P[2 * PL + off] = l4;
@@ -934,11 +965,11 @@ template <bool RK, int R>
 __device__ __forceinline__ bf16x8 frag3(const __bf16* P, int pl, int rb, int li, int lq) {
   constexpr int PL = Geo<R, RK>::PL, KRS = Geo<R, RK>::KRS;
   if constexpr (RK) {
-    return *(const bf16x8*)&P[pl * PL + (rb + li) * GX_RK + 8 * lq];
+    return *(const bf16x8*)&P[pl * PL + (rb + li) * GX_RK + 8 * (lq ^ rk_sw(li))];  // rb: a multiple of 16
   } else {
     const int tq = li >> 2, tp = li & 3;
-    return tr16_pair(&P[pl * PL + (8 * lq + tq) * KRS + rb + 4 * tp],
-                     &P[pl * PL + (8 * lq + 4 + tq) * KRS + rb + 4 * tp]);
+    return tr16_pair(&P[pl * PL + (4 * lq + tq) * KRS + rb + 4 * tp],
+                     &P[pl * PL + (16 + 4 * lq + tq) * KRS + rb + 4 * tp]);
   }
 }
 }  // namespace
@@ -1071,7 +1102,8 @@ __global__ void __launch_bounds__(256, PH == GX_FWD ? 3 : (PH == GX_GRAD ? 2 : 4
 #pragma unroll
     for (int v = 0; v < NP; ++v) {
       const int pc = t + 256 * v;
-      const int off = PH == GX_FWD ? (pc >> 2) * GX_RK + 8 * (pc & 3) : (pc / (TN / 8)) * KRSB + 8 * (pc % (TN / 8));
+      const int off = PH == GX_FWD ? (pc >> 2) * GX_RK + 8 * ((pc & 3) ^ rk_sw(pc >> 2))
+                                   : (pc / (TN / 8)) * KRSB + 8 * (pc % (TN / 8));
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<v4i*>(&Bs[pl * PLB + off]) = rbp[v][pl];
     }
@@ -1168,7 +1200,7 @@ __global__ void __launch_bounds__(256, PH == GX_FWD ? 3 : (PH == GX_GRAD ? 2 : 4
         lazy_h(rb);
       }
     }
-    blk2_store<ARK, false, TM>(ra, bnd_a(kb), As, csa);
+    blk2_store<ARK, false, TM, PH == GX_BWD>(ra, bnd_a(kb), As, csa);  // BWD: A [row][k] beside B [k][row]
     if constexpr (BP) store_bp();
     else if (want_cs) blk2_store<BRK, true, TN>(rb, bnd_b(kb), Bs, csp);
     else blk2_store<BRK, false, TN>(rb, bnd_b(kb), Bs, csp);

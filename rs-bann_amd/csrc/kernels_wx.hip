@@ -584,6 +584,12 @@ __device__ __forceinline__ bf16x8 tr16x2(const char* p0, const char* p1) {
   typedef short v8s __attribute__((ext_vector_type(8)));
   return __builtin_bit_cast(bf16x8, v8s{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]});
 }
+// f64 all-reduce over the 16 lanes of a row (fixed xor order, result in every lane)
+__device__ __forceinline__ double row_sum_d(double v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
 // two 8-byte pieces (ds_read_b64 each) as one 8-deep bf16 fragment
 __device__ __forceinline__ bf16x8 rd_pieces(const char* base, uint32_t o0, uint32_t o1) {
   const v2u a = *reinterpret_cast<const v2u*>(base + o0);
@@ -690,9 +696,15 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
   for (int u = 0; u < 4 * WX_MAXCH; ++u)
 #pragma unroll
     for (int k = 0; k < 4; ++k) dW0a[u][k] = 0.f;
-  float db0a[4], db1a[4], dW2a[4];
+  // bias gradients are column sums that cancel strongly (n-term sums of h'(z) e
+  // terms of either sign): their per-lane partials are kept in f64
+  double db0a[4], db1a[4];
+  float dW2a[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) db0a[k] = db1a[k] = dW2a[k] = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    db0a[k] = db1a[k] = 0.0;
+    dW2a[k] = 0.f;
+  }
   v4f dW1a[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
   double rss = 0.0;
 
@@ -742,7 +754,15 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
         z0[k][2] = (0x1p-11f * zs[k]) * comb4p(fa[k][2]) + c0v[k];
         z0[k][3] = (0x1p-11f * zs[k]) * comb4p(fa[k][3]) + c0v[k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) a0[k][q] = act_h_t<ACT>(z0[k][q]);
+        for (int q = 0; q < 4; ++q) {
+          if constexpr (ACT == 0) {  // z0 keeps r (tanh_r) for the derivative
+            float r;
+            a0[k][q] = tanh_r(z0[k][q], r);
+            z0[k][q] = r;
+          } else {
+            a0[k][q] = act_h_t<ACT>(z0[k][q]);
+          }
+        }
       }
     }
     // A0 planes: own half, individual 4 i + q, positions 4 g .. 4 g + 3 (hidden 16 h + 4 k + g)
@@ -773,7 +793,13 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         z1[q][r] += b1v[r];
-        a1[q][r] = act_h_t<ACT>(z1[q][r]);
+        if constexpr (ACT == 0) {  // z1 keeps r (tanh_r)
+          float rr;
+          a1[q][r] = tanh_r(z1[q][r], rr);
+          z1[q][r] = rr;
+        } else {
+          a1[q][r] = act_h_t<ACT>(z1[q][r]);
+        }
         pp[q] = fmaf(a1[q][r], w2v[r], pp[q]);
       }
     }
@@ -795,12 +821,12 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
       float sw = 0.f, sd = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        d1[q][r] = act_dh_t<ACT>(z1[q][r], a1[q][r]) * (eq[q] * w2v[r]);
+        d1[q][r] = (ACT == 0 ? dtanh_r(z1[q][r]) : act_dh_t<ACT>(z1[q][r], a1[q][r])) * (eq[q] * w2v[r]);
         sw = fmaf(a1[q][r], eq[q], sw);
         sd += d1[q][r];
       }
       dW2a[r] += sw;
-      db1a[r] += sd;
+      db1a[r] += (double)sd;
     }
     // delta1 planes: own half, individual 4 i + q, summary units 16 h + 4 g .. + 3
 #pragma unroll
@@ -821,10 +847,10 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
       for (int p = 0; p < 3; ++p) bq[p] = rd_pieces(sD + p * WX3_PLANE + 512 * q, rd_off0, rd_off1);
       const v4f acc = mm6(we3, bq, v4f{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-      for (int k = 0; k < 4; ++k) d0[k][q] = act_dh_t<ACT>(z0[k][q], a0[k][q]) * acc[k];
+      for (int k = 0; k < 4; ++k) d0[k][q] = (ACT == 0 ? dtanh_r(z0[k][q]) : act_dh_t<ACT>(z0[k][q], a0[k][q])) * acc[k];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) db0a[k] += (d0[k][0] + d0[k][1]) + (d0[k][2] + d0[k][3]);
+    for (int k = 0; k < 4; ++k) db0a[k] += (double)((d0[k][0] + d0[k][1]) + (d0[k][2] + d0[k][3]));
 
     // ---- 5. dW1 = A0^T delta1 (rows: own hidden units in position order, K = individuals) ----
 #pragma unroll
@@ -882,9 +908,9 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
   __syncthreads();  // every wave is past its last tile: the plane images are free
 
   // ---- the two pairs' accumulators, added in pair order ----
-  constexpr int NV = 4 * 4 * WX_MAXCH + 4 + 4 + 4 + 8;
+  constexpr int NV = 4 * 4 * WX_MAXCH + 4 + 8;
   float* red = reinterpret_cast<float*>(&s_img[0][0][0]);
-  double* redd = reinterpret_cast<double*>(red + 2 * NV * 64);
+  double* redd = reinterpret_cast<double*>(red + 2 * NV * 64);  // [half][9][lane]: rss, db0a, db1a
   {
     float* o = red + h * NV * 64 + lane;
     if (pr == 1) {
@@ -894,16 +920,18 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
         for (int k = 0; k < 4; ++k) o[64 * v++] = dW0a[u][k];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        o[64 * v++] = db0a[k];
-        o[64 * v++] = db1a[k];
-        o[64 * v++] = dW2a[k];
-      }
+      for (int k = 0; k < 4; ++k) o[64 * v++] = dW2a[k];
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[64 * v++] = dW1a[sb][r];
-      redd[h * 64 + lane] = rss;
+      double* od = redd + h * 9 * 64 + lane;
+      od[0] = rss;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        od[64 * (1 + k)] = db0a[k];
+        od[64 * (5 + k)] = db1a[k];
+      }
     }
     __syncthreads();
     if (pr == 1) return;
@@ -913,23 +941,25 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
       for (int k = 0; k < 4; ++k) dW0a[u][k] += o[64 * v++];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      db0a[k] += o[64 * v++];
-      db1a[k] += o[64 * v++];
-      dW2a[k] += o[64 * v++];
-    }
+    for (int k = 0; k < 4; ++k) dW2a[k] += o[64 * v++];
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) dW1a[sb][r] += o[64 * v++];
-    rss += redd[h * 64 + lane];
+    const double* od = redd + h * 9 * 64 + lane;
+    rss += od[0];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      db0a[k] += od[64 * (1 + k)];
+      db1a[k] += od[64 * (5 + k)];
+    }
   }
 
   // ---- epilogue: this half's part of the item's partial slab ----
   float* part = st.part + it.part_at;
-  float db0[4];
+  double db0[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) db0[k] = row_sum(db0a[k]);
+  for (int k = 0; k < 4; ++k) db0[k] = row_sum_d(db0a[k]);
 #pragma unroll
   for (int u = 0; u < 4 * WX_MAXCH; ++u) {
     const int j = 16 * u + i;
@@ -938,14 +968,15 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int c = 4 * (4 * h + k) + g;
-        if (c < w0) part[bd.woff[0] + c * m + j] = sg > 0.f ? (dW0a[u][k] - mu * db0[k]) / sg : 0.f;
+        if (c < w0)
+          part[bd.woff[0] + c * m + j] = sg > 0.f ? (float)(((double)dW0a[u][k] - (double)mu * db0[k]) / sg) : 0.f;
       }
     }
   }
   if (i == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (4 * (4 * h + k) + g < w0) part[bd.boff[0] + 4 * (4 * h + k) + g] = db0[k];
+      if (4 * (4 * h + k) + g < w0) part[bd.boff[0] + 4 * (4 * h + k) + g] = (float)db0[k];
   }
   // dW1 lane (n = i, g): rows 4 g + r = A0 positions 16 h + 4 g + r = hidden 16 h + 4 r + g
 #pragma unroll
@@ -958,9 +989,10 @@ __global__ void __launch_bounds__(64 * 2 * WX3_PAIRS, 2)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int s = 16 * h + 4 * g + r;
-    const float v1 = row_sum(db1a[r]), v2 = row_sum(dW2a[r]);
+    const double v1 = row_sum_d(db1a[r]);
+    const float v2 = row_sum(dW2a[r]);
     if (i == 0 && s < S) {
-      part[bd.boff[1] + s] = v1;
+      part[bd.boff[1] + s] = (float)v1;
       part[bd.woff[2] + s] = v2;
     }
   }
