@@ -504,18 +504,24 @@ def main():
         wd = threading.Timer(120.0, lambda: os._exit(0))
         wd.daemon = True
         wd.start()
-        library_comm()
-        dist.barrier()
-        t1 = time.perf_counter()
-        r = ctx.network_hmc_step(y_net, 20, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=0.1,
-                                 seed=31)
-        ctx.synchronize()
-        te = torch.tensor([time.perf_counter() - t1], device=dist_dev, dtype=torch.float64)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        if rank == 0:
-            log(json.dumps({"network_check": {"n_gpus": world, "comm": "rccl" if backend == "nccl" else backend,
-                                              "L": 20, "status": r["status"], "steps_per_s": 20 / float(te.item()),
-                                              "trace_first_last": [r["trace"][0], r["trace"][-1]]}}))
+        try:  # an error here is reported, never turned into a failed bench run (the line is out)
+            library_comm()
+            dist.barrier()
+            t1 = time.perf_counter()
+            r = ctx.network_hmc_step(y_net, 20, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=0.1,
+                                     seed=31)
+            ctx.synchronize()
+            te = torch.tensor([time.perf_counter() - t1], device=dist_dev, dtype=torch.float64)
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+            if rank == 0:
+                log(json.dumps({"network_check": {"n_gpus": world, "comm": "rccl" if backend == "nccl" else backend,
+                                                  "L": 20, "status": r["status"],
+                                                  "steps_per_s": 20 / float(te.item()),
+                                                  "trace_first_last": [r["trace"][0], r["trace"][-1]]}}))
+        except Exception as exc:  # noqa: BLE001
+            log(json.dumps({"network_check": {"rank": rank, "error": repr(exc)}}))
+            sys.stdout.flush()
+            os._exit(0)
         wd.cancel()
     ctx.close()
     if dist is not None:
