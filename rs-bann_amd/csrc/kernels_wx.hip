@@ -35,10 +35,12 @@
 //      power-of-two scale (27 significant bits); the digit image overwrites the
 //      wave's own A0^T rows (no other wave reads them after the first barrier).
 // The two waves write disjoint parts of the item's one partial slab.
-// FP32 (BF = 0): the hidden GEMMs on v_mfma_f32_16x16x4_f32 (exact f32 fmaf
-// chains, the vector rate).  BF16 (BF = 1, opt-in: C5's "bf16 hidden GEMM on
-// MFMA vs fp32"): on v_mfma_f32_16x16x32_bf16, 16x the rate, bf16 operand
-// rounding (~3e-3 relative on the hidden-layer gradients).
+// FP32 (BF = 0, BANN_WX_EXACT=1): the hidden GEMMs on v_mfma_f32_16x16x4_f32
+// (exact f32 fmaf chains, the vector rate).  BF16 (BF = 1, opt-in: C5's "bf16
+// hidden GEMM on MFMA vs fp32"): on v_mfma_f32_16x16x32_bf16, 16x the rate,
+// bf16 operand rounding (~3e-3 relative on the hidden-layer gradients).
+// The default wide kernel is k_fused_grad_wx3 below: the same phases with the
+// hidden GEMMs on the bf16 MFMA at f32 accuracy (three planes per operand).
 #include "activations.h"
 #include "bann_internal.h"
 #include "kernel_util.h"
