@@ -2,7 +2,7 @@
 # gx lazy head: (TESTS=1) GPU tests; per-phase times of one 40-branch c3def group and the
 # c3def bench line, this tree vs the builds under rs-bann_amd/ab ($VARIANTS)
 set -o pipefail
-R=$(pwd); OUT=$R/gpurun_out/r03i; mkdir -p $OUT
+R=$(pwd); OUT=$R/gpurun_out/${TAG:-gxph}; mkdir -p $OUT
 if [ -n "$TESTS" ]; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
   tail -2 $OUT/tests.log
