@@ -62,6 +62,38 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Izmailov step sizes eps = c pi / (2 sqrt(lambda) L) (ridge_ard.rs:70-117): the
+# factor c fixes the trajectory LENGTH L eps, so a c tuned at one L takes steps
+# L_ref / L times larger at a shorter L -- past the leapfrog's stability limit on
+# the stiff wide / network states (round 3: C5 at c = 0.1 accepted 0.80 at L = 20
+# but 0.0005 at L = 10).  The rule: c(L) = c_ref min(1, L / L_ref) -- below the L
+# it was tuned at, keep the tuned step size (and shorten the trajectory); above
+# it, keep the trajectory length (smaller steps).  (c_ref, L_ref) per line,
+# tuned on MI355X (tools/gpu_accept.sh):
+TUNED_FACTORS = {
+    # (config, sampler, bf16 hidden GEMM): (c_ref, L_ref)
+    ("c3", "branch", False): (1.0, 20),       # cli.rs:99-100 default c = 1
+    ("c2", "branch", False): (1.0, 20),
+    ("small", "branch", False): (1.0, 20),
+    ("c3", "sequential", False): (1.0, 20),
+    ("c3", "network", False): (0.11, 20),     # the joint state: 0.12 sits past the stiff-mode cliff
+    ("c5", "branch", False): (0.1, 20),
+    ("c5", "branch", True): (0.02, 20),       # bf16-rounded hidden activations: energy error
+    ("c3def", "branch", False): (0.02, 10),
+}
+
+
+def default_step_factor(config, sampler, bf16, L):
+    key = (config, sampler, bf16)
+    if key not in TUNED_FACTORS:   # untuned line: the branch sampler's, scaled down for the joint state
+        c, l_ref = TUNED_FACTORS.get((config, "branch", bf16), (1.0, 20))
+        if sampler == "network":
+            c *= 0.1
+    else:
+        c, l_ref = TUNED_FACTORS[key]
+    return c * min(1.0, L / l_ref)
+
+
 def init_branch_params(rng, m, widths):
     """default init (branch_cfg_builder.rs:180-186): W ~ N(0, 1/m); biases small
     random; ARD ML precisions (308-328); bias ML precisions (264-274)."""
@@ -95,6 +127,45 @@ def cpu_baseline(n, m, widths, sample_branches, sample_steps):
         return None
     branch_steps_per_s = sample_branches * sample_steps / t
     return dict(branch_steps_per_s=branch_steps_per_s, threads=threads, seconds=t, setup_s=setup.value)
+
+
+def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net, args, nb, L=20):
+    """one network-joint trajectory (bann_network_hmc_step) through the library's
+    communicator, timed per phase with HIP events: RCCL's own rank count
+    (ncclCommCount), the per-step all-reduce of the summed branch outputs, the
+    Metropolis status at the network sampler's factor for L."""
+    if ctx.comm_info()["kind"] == "none":
+        library_comm()
+    info = ctx.comm_info()
+    factor = default_step_factor(args.config, "network", args.hidden_bf16, L)
+    ctx.set_launch_timing(True)
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=factor, seed=31)
+    ctx.synchronize()
+    el = time.perf_counter() - t1
+    ctx.set_launch_timing(False)
+    fwd_ms, ar_ms, n_ar = ctx.network_timing(reset=True)
+    grad_ms, upd_ms, _ = ctx.launch_timing(reset=True)
+    vals = [el, ar_ms, fwd_ms, grad_ms, upd_ms]
+    ranks_seen = [float(info["backend_ranks"])]
+    if dist is not None:
+        import torch
+        te = torch.tensor(vals, device=dist_dev, dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        vals = [float(v) for v in te]
+        tr = torch.tensor(ranks_seen, device=dist_dev, dtype=torch.float64)
+        dist.all_reduce(tr, op=dist.ReduceOp.MIN)
+        ranks_seen = [float(tr[0])]
+    el, ar_ms, fwd_ms, grad_ms, upd_ms = vals
+    return {"n_gpus": world, "comm": info["kind"] if info["kind"] == "rccl" else f"callback ({backend})",
+            "comm_ranks_reported": int(ranks_seen[0]), "L": L, "step_factor": factor,
+            "status": {0: "accepted", 1: "rejected", 2: "rejected_early"}[r["status"]],
+            "steps_per_s": L / el, "allreduces": n_ar, "allreduce_us_per_step": 1e3 * ar_ms,
+            "allreduce_bytes": 4 * len(y_net), "forward_ms": fwd_ms, "gradient_ms": grad_ms, "update_ms": upd_ms,
+            "dH": r["trace"][-1] - r["trace"][0], "branches_per_rank": nb,
+            "timing": "HIP events on the library stream, max over ranks"}
 
 
 def launch_ranks(nproc: int) -> int:
@@ -170,8 +241,10 @@ def main():
                          "reference's own sweep order, one branch at a time against the refreshed residual "
                          "(bann_net_train, Net::train net.rs:201-358), one GPU")
     ap.add_argument("--no-network-check", action="store_true",
-                    help="N > 1: skip the short network-joint trajectory through the library's RCCL communicator "
-                         "that follows the JSON line (stderr)")
+                    help="N > 1: skip the untimed network-joint trajectory through the library's RCCL communicator "
+                         "that runs before the warmup and is reported in the line (network_check)")
+    ap.add_argument("--network-check", action="store_true",
+                    help="N = 1: run that check too, through a 1-rank RCCL communicator")
     ap.add_argument("--accept-trajectories", type=int, default=None,
                     help="untimed trajectories after the timed one whose acceptance is reported beside it "
                          "(default 4 for --sampler network: one Metropolis decision per trajectory)")
@@ -206,12 +279,7 @@ def main():
 
     n, M_total, B_total, widths = CONFIGS[args.config]
     if args.step_factor is None:
-        # C5 (W = S = 32 over 4k branches): the Izmailov sizes ignore the likelihood
-        # curvature, c = 1 rejects every trajectory; c = 0.1 accepts ~0.9 at L = 100 (tools/gpu_c5sweep.sh)
-        args.step_factor = {"c5": 0.02 if args.hidden_bf16 else 0.1, "c3def": 0.02}.get(args.config, 1.0)
-        if args.sampler == "network":   # the joint state's energy error sums over all 1000 branches
-            # 0.12 sits past the stiff-mode cliff (diverges), 0.11 accepts ~0.8
-            args.step_factor = {"c3": 0.11}.get(args.config, 0.1 * args.step_factor)
+        args.step_factor = default_step_factor(args.config, args.sampler, args.hidden_bf16, args.steps)
     heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
     if args.cpu_sample_branches is None:
         args.cpu_sample_branches = 4 if heavy else 96
@@ -280,8 +348,10 @@ def main():
     def library_comm():
         """the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
         all-reduce callback when rehearsing N ranks on one GPU"""
-        import torch
-        if backend == "nccl":
+        if dist is None:   # one rank: a 1-rank RCCL communicator (--network-check)
+            ctx.comm_init_rccl(comm_unique_id(), 1, 0)
+        elif backend == "nccl":
+            import torch
             idt = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local_rank}")
             if rank == 0:
                 idt.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
@@ -289,7 +359,7 @@ def main():
             ctx.comm_init_rccl(bytes(idt.cpu().numpy()), world, rank)
         else:
             ctx.comm_callback(TorchAllreduce(dist), world, rank)
-        torch.cuda.synchronize()
+        ctx.synchronize()
 
     if dist is not None and args.sampler == "network":   # the per-step all-reduce needs it in the timed region
         library_comm()
@@ -331,6 +401,31 @@ def main():
         ctx.leapfrog_steps(L)
         status, acc = ctx.leapfrog_end()
         return acc
+
+    # C4's collective, checked before anything is timed and reported INSIDE the
+    # line: one network-joint trajectory through the library's communicator (RCCL
+    # over xGMI at N > 1: the per-step all-reduce of the summed branch outputs),
+    # from the generating state (y = sum_b f_b + noise), at the network sampler's
+    # factor for its L.  A stalled collective ends the run with a non-zero exit
+    # (watchdog), an error likewise; the line is never printed without it.
+    netcheck = None
+    if args.sampler == "branch" and not args.no_network_check and (dist is not None or args.network_check):
+        import threading
+        wd = threading.Timer(180.0, lambda: (log(f"network_check: rank {rank}: collective stalled"), os._exit(3)))
+        wd.daemon = True
+        wd.start()
+        try:
+            netcheck = network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net, args, nb)
+        except Exception as exc:  # noqa: BLE001
+            log(f"network_check: rank {rank}: {exc!r}")
+            sys.stdout.flush()
+            os._exit(4)
+        wd.cancel()
+        if rank == 0:
+            log(json.dumps({"network_check": netcheck}))
+        if netcheck["status"] != "accepted":   # back at theta_0: the sweep-start targets again
+            ctx.residual_set(noise.astype(np.float32))
+            ctx.rebuild_targets(branches)
 
     # warmup: a full trajectory of W steps (loads every kernel), then the
     # roofline's back-to-back launch timing (bann_profile_session: a 2-step
@@ -492,37 +587,11 @@ def main():
             "step_factor": args.step_factor,
             "setup_s": setup_s,
         }
+        if netcheck is not None:
+            out["network_check"] = netcheck
         if args.emulate_shard:
             out["emulated_shard_of"] = args.emulate_shard   # not a whole-job number: one rank's shard
         print(json.dumps(out), flush=True)
-    if dist is not None and args.sampler == "branch" and not args.no_network_check:
-        # after the line: one short network-joint trajectory through the library's
-        # communicator (RCCL over xGMI: the per-step all-reduce of the summed branch
-        # outputs, config C4's collective), reported on stderr.  A watchdog ends the
-        # process if the collective stalls, so the line above is never lost.
-        import threading
-        wd = threading.Timer(120.0, lambda: os._exit(0))
-        wd.daemon = True
-        wd.start()
-        try:  # an error here is reported, never turned into a failed bench run (the line is out)
-            library_comm()
-            dist.barrier()
-            t1 = time.perf_counter()
-            r = ctx.network_hmc_step(y_net, 20, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=0.1,
-                                     seed=31)
-            ctx.synchronize()
-            te = torch.tensor([time.perf_counter() - t1], device=dist_dev, dtype=torch.float64)
-            dist.all_reduce(te, op=dist.ReduceOp.MAX)
-            if rank == 0:
-                log(json.dumps({"network_check": {"n_gpus": world, "comm": "rccl" if backend == "nccl" else backend,
-                                                  "L": 20, "status": r["status"],
-                                                  "steps_per_s": 20 / float(te.item()),
-                                                  "trace_first_last": [r["trace"][0], r["trace"][-1]]}}))
-        except Exception as exc:  # noqa: BLE001
-            log(json.dumps({"network_check": {"rank": rank, "error": repr(exc)}}))
-            sys.stdout.flush()
-            os._exit(0)
-        wd.cancel()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -260,6 +260,11 @@ int bann_synchronize(bann_ctx* ctx);
  * (Set outside a session.) */
 int bann_set_launch_timing(bann_ctx* ctx, int32_t enabled);
 int bann_launch_timing(bann_ctx* ctx, float* grad_ms, float* update_ms, int32_t* grad_launches, int32_t reset);
+/* the same timing inside bann_network_hmc_step (whose gradient and update
+ * launches also count in bann_launch_timing): average milliseconds of the
+ * forward-only launch and of the per-step all-reduce of the summed branch
+ * outputs (RCCL, or the callback's host round trip), and the all-reduce count */
+int bann_network_timing(bann_ctx* ctx, float* forward_ms, float* allreduce_ms, int32_t* allreduces, int32_t reset);
 /* individuals n of the context's cohort */
 int64_t bann_ctx_num_individuals(const bann_ctx* ctx);
 /* measurement hook: times `iters` packed gradient launches and `iters` update
@@ -319,6 +324,10 @@ int bann_comm_unique_id(uint8_t* id_out);
 int bann_ctx_comm_init(bann_ctx* ctx, const uint8_t* id, int32_t nranks, int32_t rank);
 /* a caller-provided all-reduce on host buffers instead of RCCL */
 int bann_ctx_comm_callback(bann_ctx* ctx, bann_allreduce_fn fn, void* user, int32_t nranks, int32_t rank);
+/* the context's communicator: kind 0 none, 1 RCCL, 2 callback; its rank count
+ * and rank; backend_ranks = the rank count RCCL itself reports (ncclCommCount)
+ * for kind 1, else nranks.  Outputs may be NULL. */
+int bann_comm_info(const bann_ctx* ctx, int32_t* kind, int32_t* nranks, int32_t* rank, int32_t* backend_ranks);
 /* residual bookkeeping over ranks on the host: local_delta is summed over the
  * ranks in place, then residual[i] -= local_delta[i].  The exchange step of
  * bann_exchange_residual for a callback communicator.  Host only. */

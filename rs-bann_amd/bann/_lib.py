@@ -120,6 +120,7 @@ SIGNATURES = {
     "bann_comm_unique_id": (C.c_int, [_pu8]),
     "bann_ctx_comm_init": (C.c_int, [_P, _pu8, _i32, _i32]),
     "bann_ctx_comm_callback": (C.c_int, [_P, ALLREDUCE_FN, _P, _i32, _i32]),
+    "bann_comm_info": (C.c_int, [_P, _pi32, _pi32, _pi32, _pi32]),
     "bann_residual_update_host": (C.c_int, [ALLREDUCE_FN, _P, _pf32, _pf32, _i64]),
     "bann_exchange_residual": (C.c_int, [_P, _pf32]),
     "bann_network_hmc_step": (C.c_int, [_P, _pf32, _f32, _f32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32,
@@ -136,6 +137,7 @@ SIGNATURES = {
     "bann_rebuild_targets": (C.c_int, [_P, _pi32, _i32, _P]),
     "bann_set_launch_timing": (C.c_int, [_P, _i32]),
     "bann_launch_timing": (C.c_int, [_P, _pf32, _pf32, _pi32, _i32]),
+    "bann_network_timing": (C.c_int, [_P, _pf32, _pf32, _pi32, _i32]),
     "bann_ctx_num_individuals": (_i64, [_P]),
     "bann_leapfrog_begin": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _u64]),
     "bann_leapfrog_steps": (C.c_int, [_P, _i32]),

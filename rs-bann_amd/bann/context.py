@@ -312,6 +312,14 @@ class BannContext:
         self._allreduce = allreduce   # the library keeps the function pointer
         self._check(self._lib.bann_ctx_comm_callback(self._h, allreduce.fn, None, nranks, rank))
 
+    def comm_info(self) -> dict:
+        """the context's communicator: kind ("none" / "rccl" / "callback"), ranks, rank and
+        the rank count the backend itself reports (ncclCommCount for RCCL)."""
+        k, nr, r, br = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        self._check(self._lib.bann_comm_info(self._h, C.byref(k), C.byref(nr), C.byref(r), C.byref(br)))
+        return dict(kind={0: "none", 1: "rccl", 2: "callback"}[k.value], nranks=nr.value, rank=r.value,
+                    backend_ranks=br.value)
+
     def exchange_residual(self, residual) -> np.ndarray:
         """residual -= sum over ranks of the last session's residual change (collective)."""
         res = np.ascontiguousarray(residual, dtype=np.float32).copy()
@@ -400,6 +408,12 @@ class BannContext:
         g, u, k = C.c_float(), C.c_float(), C.c_int32()
         self._check(self._lib.bann_launch_timing(self._h, C.byref(g), C.byref(u), C.byref(k), 1 if reset else 0))
         return g.value, u.value, k.value
+
+    def network_timing(self, reset: bool = True):
+        """(forward_ms, allreduce_ms, allreduces): averages over the timed network-mode steps."""
+        f, a, k = C.c_float(), C.c_float(), C.c_int32()
+        self._check(self._lib.bann_network_timing(self._h, C.byref(f), C.byref(a), C.byref(k), 1 if reset else 0))
+        return f.value, a.value, k.value
 
     # ------------------------------------------------------ leapfrog session
     def leapfrog_begin(self, branches: Sequence[int], L: int, max_hamiltonian_error: float = 10.0,

@@ -1553,9 +1553,10 @@ extern "C" int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap,
 }
 
 // ---- in-trajectory launch timing (bann_set_launch_timing) ----
-// an event after every launch boundary of the session: kind 0 before a gradient
-// launch, 1 between the gradient and the update launch, 2 after the update
-static void tm_mark(bann_ctx* ctx, int32_t kind) {
+// an event at every launch boundary: TM_GRAD0 before a gradient launch, TM_GRAD1
+// between the gradient and the update launch, TM_UPD1 after the update; network
+// mode adds TM_FWD0/1 around the forward launch and TM_AR0/1 around the all-reduce
+void tm_mark(bann_ctx* ctx, int32_t kind) {
   if (!ctx->tm_on) return;
   const size_t k = ctx->tm_marks.size();
   if (k == ctx->tm_pool.size()) {
@@ -1567,20 +1568,21 @@ static void tm_mark(bann_ctx* ctx, int32_t kind) {
   ctx->tm_marks.push_back({(int32_t)k, kind});
 }
 
-// after the stream has drained: elapsed times of the gradient (0 -> 1) and update (1 -> 2) launches
-static int tm_resolve(bann_ctx* ctx) {
+// after the stream has drained: elapsed time of every (start, end) pair of marks
+int tm_resolve(bann_ctx* ctx) {
   for (size_t i = 0; i + 1 < ctx->tm_marks.size(); ++i) {
     const auto a = ctx->tm_marks[i], b = ctx->tm_marks[i + 1];
-    if (!((a.second == 0 && b.second == 1) || (a.second == 1 && b.second == 2))) continue;
+    double* acc = nullptr;
+    int32_t* cnt = nullptr;
+    if (a.second == TM_GRAD0 && b.second == TM_GRAD1) acc = &ctx->tm_grad_ms, cnt = &ctx->tm_grad_n;
+    else if (a.second == TM_GRAD1 && b.second == TM_UPD1) acc = &ctx->tm_upd_ms, cnt = &ctx->tm_upd_n;
+    else if (a.second == TM_FWD0 && b.second == TM_FWD1) acc = &ctx->tm_fwd_ms, cnt = &ctx->tm_fwd_n;
+    else if (a.second == TM_AR0 && b.second == TM_AR1) acc = &ctx->tm_ar_ms, cnt = &ctx->tm_ar_n;
+    if (!acc) continue;
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, ctx->tm_pool[a.first], ctx->tm_pool[b.first]));
-    if (a.second == 0) {
-      ctx->tm_grad_ms += ms;
-      ++ctx->tm_grad_n;
-    } else {
-      ctx->tm_upd_ms += ms;
-      ++ctx->tm_upd_n;
-    }
+    *acc += ms;
+    ++*cnt;
   }
   ctx->tm_marks.clear();
   return BANN_OK;
@@ -1607,6 +1609,19 @@ extern "C" int bann_launch_timing(bann_ctx* ctx, float* grad_ms, float* update_m
   return BANN_OK;
 }
 
+extern "C" int bann_network_timing(bann_ctx* ctx, float* forward_ms, float* allreduce_ms, int32_t* allreduces,
+                                   int32_t reset) {
+  if (!ctx) return BANN_E_ARG;
+  if (forward_ms) *forward_ms = ctx->tm_fwd_n ? (float)(ctx->tm_fwd_ms / ctx->tm_fwd_n) : 0.f;
+  if (allreduce_ms) *allreduce_ms = ctx->tm_ar_n ? (float)(ctx->tm_ar_ms / ctx->tm_ar_n) : 0.f;
+  if (allreduces) *allreduces = ctx->tm_ar_n;
+  if (reset) {
+    ctx->tm_fwd_ms = ctx->tm_ar_ms = 0.0;
+    ctx->tm_fwd_n = ctx->tm_ar_n = 0;
+  }
+  return BANN_OK;
+}
+
 extern "C" int64_t bann_ctx_num_individuals(const bann_ctx* ctx) { return ctx ? ctx->n : BANN_E_ARG; }
 
 extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
@@ -1623,12 +1638,12 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
   }
   rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
   if (rc) return rc;
-  tm_mark(ctx, 0);
+  tm_mark(ctx, TM_GRAD0);
   rc = run_grad(ctx, ctx->lf, 2);  // f(theta_0) straight into pred0 (the restore copy and the residual change)
   if (rc) return rc;
-  tm_mark(ctx, 1);
+  tm_mark(ctx, TM_GRAD1);
   run_update(ctx, ctx->lf, MODE_INIT, 0);
-  tm_mark(ctx, 2);
+  tm_mark(ctx, TM_UPD1);
   CK(hipGetLastError());
   ctx->lf_active = true;
   ctx->lf_L = L;
@@ -1641,12 +1656,12 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   if (k < 0 || ctx->lf_step + k > ctx->lf_L) return fail(ctx, BANN_E_ARG, "steps beyond the trajectory length");
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
-    tm_mark(ctx, 0);
+    tm_mark(ctx, TM_GRAD0);
     int rc = run_grad(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0);
     if (rc) return rc;
-    tm_mark(ctx, 1);
+    tm_mark(ctx, TM_GRAD1);
     run_update(ctx, ctx->lf, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
-    tm_mark(ctx, 2);
+    tm_mark(ctx, TM_UPD1);
   }
   CK(hipGetLastError());
   return BANN_OK;

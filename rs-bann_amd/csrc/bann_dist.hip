@@ -75,6 +75,22 @@ extern "C" int bann_ctx_comm_init(bann_ctx* ctx, const uint8_t* id, int32_t nran
   return BANN_OK;
 }
 
+extern "C" int bann_comm_info(const bann_ctx* ctx, int32_t* kind, int32_t* nranks, int32_t* rank,
+                               int32_t* backend_ranks) {
+  if (!ctx) return BANN_E_ARG;
+  int32_t count = ctx->comm_kind == 0 ? 1 : ctx->nranks;
+  if (ctx->comm_kind == 1) {  // RCCL's own view of the communicator
+    int c = 0;
+    if (ncclCommCount((ncclComm_t)ctx->nccl, &c) != ncclSuccess) return BANN_E_HIP;
+    count = c;
+  }
+  if (kind) *kind = ctx->comm_kind;
+  if (nranks) *nranks = ctx->comm_kind == 0 ? 1 : ctx->nranks;
+  if (rank) *rank = ctx->comm_kind == 0 ? 0 : ctx->rank;
+  if (backend_ranks) *backend_ranks = count;
+  return BANN_OK;
+}
+
 extern "C" int bann_ctx_comm_callback(bann_ctx* ctx, bann_allreduce_fn fn, void* user, int32_t nranks, int32_t rank) {
   if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks) return BANN_E_ARG;
   comm_destroy(ctx);
@@ -204,27 +220,40 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   ctx->st.netmode = 1;
   ctx->st.net_le = lambda_e;
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
+  // (launch timing, when enabled: forward, all-reduce, gradient and update spans)
   auto forward_and_targets = [&](int k) -> int {
+    tm_mark(ctx, TM_FWD0);
     int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
     if (r) return r;
+    tm_mark(ctx, TM_FWD1);
     launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
+    tm_mark(ctx, TM_AR0);
     r = allreduce_device_f32(ctx, ctx->d_netsum, n);
     if (r) return r;
+    tm_mark(ctx, TM_AR1);
     launch_net_targets(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart, ctx->d_netrss + k,
                        ctx->stream);
-    return run_grad(ctx, p, 0);
+    tm_mark(ctx, TM_GRAD0);
+    r = run_grad(ctx, p, 0);
+    tm_mark(ctx, TM_GRAD1);
+    return r;
   };
   rc = forward_and_targets(0);
   if (!rc) {
     launch_snapshot_pred(ctx->st, p.d_all, nb, ctx->stream);
     run_update(ctx, p, MODE_INIT, 0);
+    tm_mark(ctx, TM_UPD1);
     for (int k = 1; k <= L && !rc; ++k) {
       rc = forward_and_targets(k);
       if (!rc) run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
+      tm_mark(ctx, TM_UPD1);
     }
   }
   ctx->st.netmode = 0;
-  if (rc) return rc;
+  if (rc) {
+    ctx->tm_marks.clear();
+    return rc;
+  }
   CK(hipGetLastError());
   // network -H per step: sum over local branches (list order) and ranks, plus the rss term once.
   // The Metropolis uniform rides along as entry L + 1: rank 0's draw (or the
@@ -233,6 +262,8 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   CK(hipMemcpyAsync(tr.data(), ctx->d_htrace, tr.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipMemcpyAsync(rss.data(), ctx->d_netrss, (L + 1) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
+  rc = tm_resolve(ctx);
+  if (rc) return rc;
   for (int k = 0; k <= L; ++k)
     for (int b = 0; b < nb; ++b) H[k] += tr[(size_t)b * ctx->htrace_cap + k];
   if (ctx->rank == 0) {

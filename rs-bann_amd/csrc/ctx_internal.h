@@ -133,9 +133,10 @@ struct bann_ctx {
   // gradient and update launch of the leapfrog sessions, resolved at bann_leapfrog_end
   bool tm_on = false;
   std::vector<hipEvent_t> tm_pool;
-  std::vector<std::pair<int32_t, int32_t>> tm_marks;  // (event index, kind: 0 before grad, 1 after grad, 2 after update)
-  double tm_grad_ms = 0.0, tm_upd_ms = 0.0;
-  int32_t tm_grad_n = 0, tm_upd_n = 0;
+  // (event index, kind): TM_* below; a sample is the span between a kind and its successor kind
+  std::vector<std::pair<int32_t, int32_t>> tm_marks;
+  double tm_grad_ms = 0.0, tm_upd_ms = 0.0, tm_fwd_ms = 0.0, tm_ar_ms = 0.0;
+  int32_t tm_grad_n = 0, tm_upd_n = 0, tm_fwd_n = 0, tm_ar_n = 0;
   // trajectory recording (mcmc_cfg.trajectories, trajectory.rs): per branch of the last bann_hmc_step
   bool rec_on = false;
   struct Rec {
@@ -195,3 +196,7 @@ void launch_residual_sub(float* r, const float* d, int64_t n, hipStream_t s);
 void mark_predictions(bann_ctx* ctx, const Plan& p, bool current);
 int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t step_mode, float factor,
                  const float* eps, const float* momentum, uint64_t seed, const float* u);
+// in-trajectory launch timing (bann_set_launch_timing): event marks on the context stream
+enum { TM_GRAD0 = 0, TM_GRAD1 = 1, TM_UPD1 = 2, TM_AR0 = 3, TM_AR1 = 4, TM_FWD0 = 5, TM_FWD1 = 6 };
+void tm_mark(bann_ctx* ctx, int32_t kind);
+int tm_resolve(bann_ctx* ctx);  // after the stream has drained

@@ -133,3 +133,67 @@ def test_network_hmc_two_ranks_match_one(u):
     params = two[0]["params"] + two[1]["params"]
     for b, pv in enumerate(params):
         assert norm_rel(pv, one["params"][b]) < 1e-5, b
+
+
+def test_rccl_one_rank_communicator():
+    """the library's RCCL communicator (bann_comm_unique_id + bann_ctx_comm_init)
+    at world size 1, on the GPU: RCCL reports one rank, and every collective path
+    -- the network trajectory's per-step f32 all-reduce of the summed branch
+    outputs, its f64 -H / uniform all-reduce, and the device residual exchange
+    of a leapfrog session -- gives the bits of the same calls with no
+    communicator, and the oracle's trajectory."""
+    from bann.distributed import comm_unique_id
+    rng, g, specs = _problem(seed=13)
+    n, L = g.shape[1], 5
+    plain = _context(g, specs, range(len(specs)))
+    rccl = _context(g, specs, range(len(specs)))
+    assert plain.comm_info()["kind"] == "none"
+    rccl.comm_init_rccl(comm_unique_id(), 1, 0)
+    info = rccl.comm_info()
+    assert info == dict(kind="rccl", nranks=1, rank=0, backend_ranks=1), info
+    mu, sd = plain.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    y = rng.normal(size=n).astype(np.float32)
+    eps, mom = _draws(rng, specs, L)
+    # injected draws: both contexts and the oracle
+    brs = [s["branch"].copy() for s in specs]
+    rccl.set_launch_timing(True)
+    r0 = plain.network_hmc_step(y, L, bias=0.1, lambda_e=0.9, eps=np.concatenate(eps), momentum=np.concatenate(mom),
+                                u=0.3)
+    r1 = rccl.network_hmc_step(y, L, bias=0.1, lambda_e=0.9, eps=np.concatenate(eps), momentum=np.concatenate(mom),
+                               u=0.3)
+    rccl.set_launch_timing(False)
+    fwd_ms, ar_ms, n_ar = rccl.network_timing()
+    assert n_ar == L + 1 and ar_ms > 0.0 and fwd_ms > 0.0, (fwd_ms, ar_ms, n_ar)
+    assert r0["status"] == r1["status"] and np.array_equal(r0["trace"], r1["trace"]), (r0, r1)
+    out = O.network_hmc_step(brs, Xs, y.astype(np.float64), 0.1, 0.9, [e.astype(np.float64) for e in eps],
+                             [p.astype(np.float64) for p in mom], L, 10.0, 0.3)
+    assert r1["status"] == out["status"]
+    tr = np.asarray(out["trace"])
+    assert np.all(np.abs(r1["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr)))
+    for b, br in enumerate(brs):
+        assert np.array_equal(plain.get_params(b), rccl.get_params(b)), b
+        assert norm_rel(rccl.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+    # library-drawn momenta and uniform (rank 0's draw shared through the f64 all-reduce)
+    r0 = plain.network_hmc_step(y, L, bias=0.1, lambda_e=0.9, step_factor=0.3, seed=21)
+    r1 = rccl.network_hmc_step(y, L, bias=0.1, lambda_e=0.9, step_factor=0.3, seed=21)
+    assert r0["status"] == r1["status"] and np.array_equal(r0["trace"], r1["trace"])
+    # a leapfrog session, then the residual exchange on the device (RCCL sum over one rank)
+    all_b = list(range(len(specs)))
+    for ctx in (plain, rccl):
+        ctx.residual_set(y)
+        ctx.rebuild_targets(all_b)
+        ctx.leapfrog_begin(all_b, 4, 10.0, "izmailov", 0.3, seed=5)
+        ctx.leapfrog_steps(4)
+        ctx.leapfrog_end()
+    d0 = plain.residual_delta()
+    plain.exchange_residual_device()
+    rccl.exchange_residual_device()
+    res0, res1 = plain.residual_get(), rccl.residual_get()
+    assert np.array_equal(res0, res1)
+    assert np.array_equal(res0, y - d0)
+    assert np.any(d0 != 0.0)   # something was accepted: the exchange moved the residual
+    # host-residual variant through the RCCL device sum
+    assert np.array_equal(plain.exchange_residual(y), rccl.exchange_residual(y))
+    plain.close()
+    rccl.close()
