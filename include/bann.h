@@ -166,6 +166,26 @@ int bann_rss(bann_ctx* ctx, int32_t b, double* rss_out);
  * log_density_gradient_wrt_biases 322-331); grad_out in param_vec order.
  * rss_out (optional) receives the rss at the same parameters (823-828). */
 int bann_log_density_gradient(bann_ctx* ctx, int32_t b, float* grad_out, double* rss_out);
+/* the same for several branches from ONE packed gradient launch, each against
+ * its own current target (Net::gradient, net.rs:520-527, sets every target to
+ * the phenotype first): grad_out = the branches' param_vec gradients
+ * concatenated in list order, rss_out[nb] (may be NULL) */
+int bann_log_density_gradient_many(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* grad_out,
+                                   double* rss_out);
+/* log_density_gradient_joint (branch_sampler.rs:406-422) at the branch's current
+ * parameters and precision vector: grad_out[P + Q] = [params | precisions]
+ * (ridge_ard.rs:221-250 etc.), the rss and the joint log density
+ * (log_density_joint, 292-305; the output-weight stat of bann_branch_set_output_stats).
+ * hyper: 6 floats as bann_hmc_step_joint.  rss_out / log_density_out may be NULL. */
+int bann_log_density_gradient_joint(bann_ctx* ctx, int32_t b, const float* hyper, float* grad_out, double* rss_out,
+                                    double* log_density_out);
+/* forward_feed (branch_sampler.rs:743-782) keeping every layer, for
+ * Net::activations (net.rs:509-518): act_out = the activations of layer 0, 1,
+ * ..., L-1 (the last one is the output), each [w_l][n] column-major (element
+ * (i, k) at k n + i), sum_l w_l n floats; pre_out (may be NULL) = the
+ * pre-activations of the hidden and summary layers (the output's equals its
+ * activation and is not repeated), sum_{l<L-1} w_l n floats. */
+int bann_forward_feed(bann_ctx* ctx, int32_t b, float* pre_out, float* act_out);
 /* log_density (branch_sampler.rs:72-78; std_normal_branch.rs:149-158) at the
  * current parameters and the given rss */
 int bann_log_density(bann_ctx* ctx, int32_t b, double rss, double* out);
@@ -204,6 +224,13 @@ int bann_set_trajectory_recording(bann_ctx* ctx, int32_t enabled);
  * hamiltonian[steps + 1]; at most cap steps are copied; outputs may be NULL */
 int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap, int32_t* steps, float* params, float* ldg,
                                double* hamiltonian);
+/* the same for a trajectory recorded by bann_hmc_step_joint (the joint
+ * Trajectory of branch_sampler.rs:1126-1135): per step the parameters [P], the
+ * precisions [Q] (precision_vec order) and the joint log-density gradient
+ * [P + Q] (params | precisions); hamiltonian = the joint -H trace.  Each call
+ * refuses the other kind of recording (BANN_E_STATE). */
+int bann_branch_get_trajectory_joint(bann_ctx* ctx, int32_t b, int32_t cap, int32_t* steps, float* params,
+                                     float* precisions, float* ldg, double* hamiltonian);
 
 /* ---------------- joint HMC: replaces hmc_step_joint (branch_sampler.rs:1070-1178) ----------------
  * One trajectory per listed branch over its parameters AND its precisions
@@ -378,6 +405,10 @@ const char* bann_fused_kernel_name(void);
  * BASELINE config C5's "bf16 hidden GEMM on MFMA vs fp32": bf16 operand
  * rounding (~1e-3 relative on gradients; not parity-exact).  Any time. */
 int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled);
+/* replay a trajectory's whole launch sequence as one captured HIP graph in
+ * bann_hmc_step (1) or launch kernel by kernel (0; default, or BANN_HMC_GRAPH);
+ * the same launches, the same bits.  Trajectory recording always launches. */
+int bann_set_graph_replay(bann_ctx* ctx, int32_t enabled);
 /* force every branch onto the layered gx path (0) or allow the fused kernels (1) */
 int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
 /* bytes of packed genotype data read per full gradient evaluation of all branches */

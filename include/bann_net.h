@@ -63,6 +63,13 @@ typedef struct {
   int32_t trajectories;  /* outdir/traj: one JSON Trajectory line per HMC step (trajectory.rs, branch_sampler.rs:1196-1289) */
   int32_t joint_hmc;     /* MCMCCfg::joint_hmc: hmc_step_joint over params and precisions, no Gibbs draws
                             (net.rs:270-290; random step sizes, branch_sampler.rs:1092-1101) */
+  int32_t gradient_descent;        /* MCMCCfg::gradient_descent (takes precedence, net.rs:282-290):
+                                      BranchSampler::gradient_descent (branch_sampler.rs:964-1002), L ascent
+                                      steps with a doubling / halving rss line search from the step size
+                                      factor; Gibbs draws as HMC; always accepted; no trajectories */
+  int32_t gradient_descent_joint;  /* MCMCCfg::gradient_descent_joint: gradient_descent_joint (1019-1066), L
+                                      ascent steps of params and precisions at the step size factor, no Gibbs
+                                      draws; rejected if the error precision ends <= 0 */
 } bann_mcmc_cfg;
 
 /* Host random source for the driver's draws (the reference's ThreadRng,
@@ -137,6 +144,21 @@ int bann_net_perturb(bann_net* net, int32_t has_params, float params_by, int32_t
  * widths) -- e.g. a test cohort -- or NULL for the net's own context.  The net's
  * current parameters are loaded into ctx first. */
 int bann_net_predict(bann_net* net, bann_ctx* ctx, float* y_hat_out);
+/* Net::rss / Net::mse (net.rs:637-646) on the cohort of ctx (NULL: the net's own)
+ * against y[n]: sum (y - y_hat)^2 with y_hat of bann_net_predict; mse = rss / n */
+int bann_net_rss(bann_net* net, bann_ctx* ctx, const float* y, int64_t n, double* rss_out);
+/* Net::gradient (net.rs:520-527): every branch's log_density_gradient against
+ * the phenotype y[n] itself (not the residual), at the net's parameters and
+ * precisions, one packed launch; grad_out = the branches' param_vecs
+ * concatenated in branch order.  ctx: a context with the net's branches or NULL
+ * (the net's own, whose branch targets this overwrites). */
+int bann_net_gradient(bann_net* net, bann_ctx* ctx, const float* y, int64_t n, float* grad_out);
+/* Net::branch_r2s (net.rs:648-656, r2 = 1 - rss(x_b, y) / sum y^2,
+ * branch_sampler.rs:911-913) for every branch against y[n]; ctx as above */
+int bann_net_branch_r2s(bann_net* net, bann_ctx* ctx, const float* y, int64_t n, float* r2_out);
+/* Net::activations (net.rs:509-518) of branch b: forward_feed's activations of
+ * every layer at the net's parameters (bann_forward_feed layout); ctx as above */
+int bann_net_activations(bann_net* net, bann_ctx* ctx, int32_t b, float* act_out);
 int bann_net_summary(const bann_net* net, bann_train_summary* out);
 /* the recorded mse_train / lpd series (TrainingStats::mse_train / lpd);
  * writes min(cap, num_records) entries of each (either may be NULL) */

@@ -618,6 +618,7 @@ def hmc_step_joint(br: Branch, X, y, hp: Hyper, eps, p, L_int: int, max_dH: floa
     H0 = neg_h()
     g, _ = ldg_joint_vec(br, X, y, hp)
     trace = [H0]
+    states, ldgs = [], []   # the joint Trajectory (1126-1135): state and ldg after every step
     for step in range(L_int):
         p += 0.5 * eps * g                                             # 1114
         set_state(state() + eps * p)                                   # 1115-1116
@@ -626,20 +627,81 @@ def hmc_step_joint(br: Branch, X, y, hp: Hyper, eps, p, L_int: int, max_dH: floa
         p += 0.5 * eps * g                                             # 1119
         H = neg_h()                                                    # 1123-1124
         trace.append(H)
+        states.append(state())
+        ldgs.append(g.copy())
         if abs(H - H0) > max_dH:                                       # 1138-1158 (NaN never exceeds)
             br.weights, br.biases = init.weights, init.biases
             load_precision_vec(br, precision_vec(init))
-            return dict(status=REJECTED_EARLY, trace=trace, step=step)
+            return dict(status=REJECTED_EARLY, trace=trace, step=step, states=states, ldgs=ldgs)
     r = predict(br, X) - y
     with np.errstate(all="ignore"):
         ld = log_density(br, float(np.sum(r * r)))                     # non-joint (943)
         log_acc = (ld - 0.5 * float(p @ p)) - H0
         acc_p = 1.0 if log_acc >= 0 else math.exp(log_acc)
     if u < acc_p:
-        return dict(status=ACCEPTED, trace=trace, log_density=ld, p=p)
+        return dict(status=ACCEPTED, trace=trace, log_density=ld, p=p, states=states, ldgs=ldgs)
     br.weights, br.biases = init.weights, init.biases
     load_precision_vec(br, precision_vec(init))
-    return dict(status=REJECTED, trace=trace, log_density=ld, p=p)
+    return dict(status=REJECTED, trace=trace, log_density=ld, p=p, states=states, ldgs=ldgs)
+
+
+def gradient_descent(br: Branch, X, y, factor: float, L_int: int):
+    """BranchSampler::gradient_descent (branch_sampler.rs:964-1002): L ascent steps
+    theta += s * ldg (descend_gradient, params.rs:740-749), s from a doubling /
+    halving line search over rss probes from the step size factor
+    (probe_gradient_step, 1004-1016); always accepted.  ``br`` moves in place."""
+    th = param_vec(br.weights, br.biases)
+
+    def set_th(v):
+        br.weights, br.biases = load_param_vec(v, br.num_markers, br.layer_widths)
+
+    def grad():
+        gw, gb, _ = log_density_gradient(br, X, y)
+        return param_vec(gw, gb)
+
+    def probe(step):
+        set_th(th + step * g)
+        return rss(br, X, y)
+
+    g = grad()
+    for _ in range(L_int):
+        step = float(np.float32(factor))
+        prev = probe(step)
+        f = 2.0 if probe(2.0 * step) < prev else 0.5
+        step *= f
+        curr = probe(step)
+        guard = 0
+        while curr < prev and guard < 4096:
+            prev = curr
+            step *= f
+            curr = probe(step)
+            guard += 1
+        step /= f
+        th = th + step * g
+        set_th(th)
+        g = grad()
+    set_th(th)
+    return dict(status=ACCEPTED)
+
+
+def gradient_descent_joint(br: Branch, X, y, hp: "Hyper", factor: float, L_int: int):
+    """BranchSampler::gradient_descent_joint (branch_sampler.rs:1019-1066): L steps
+    of params and precisions along the joint log-density gradient at the fixed
+    factor; rejected (restored) if the error precision ends <= 0."""
+    P = br.num_params
+    init = br.copy()
+    g, _ = ldg_joint_vec(br, X, y, hp)
+    for _ in range(L_int):
+        v = np.concatenate([param_vec(br.weights, br.biases), precision_vec(br)]) + float(np.float32(factor)) * g
+        br.weights, br.biases = load_param_vec(v[:P], br.num_markers, br.layer_widths)
+        load_precision_vec(br, v[P:])
+        with np.errstate(all="ignore"):
+            g, _ = ldg_joint_vec(br, X, y, hp)
+    if not (br.error_precision > 0.0):
+        br.weights, br.biases = init.weights, init.biases
+        load_precision_vec(br, precision_vec(init))
+        return dict(status=REJECTED)
+    return dict(status=ACCEPTED)
 
 
 # --------------------------------------------------------------------------

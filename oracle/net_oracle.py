@@ -112,9 +112,11 @@ class NetOracle:
 
     def train(self, y, d: Draws, chain_length: int, L_int: int, max_dH: float = 10.0, factor: float = 1.0,
               step_mode: str = "izmailov", fixed_param_precisions: bool = False, sampled_output_bias: bool = False,
-              joint_hmc: bool = False, single_branch: bool = False):
-        """Net::train (net.rs:201-358), HMC path; single_branch: Net::train_single_branch
-        (net.rs:360-507: branch 0 every chain iteration, a record after every update)."""
+              joint_hmc: bool = False, single_branch: bool = False, gradient_descent: bool = False,
+              gradient_descent_joint: bool = False):
+        """Net::train (net.rs:201-358); single_branch: Net::train_single_branch
+        (net.rs:360-507: branch 0 every chain iteration, a record after every update).
+        The step (282-290): gradient descent, joint gradient descent, joint HMC, HMC."""
         n = y.size
         nb = len(self.br)
         k_out, s_out = self.hp.output
@@ -136,7 +138,7 @@ class NetOracle:
             for b in order:
                 br = self.br[b]
                 others = self._from_cfg(b)
-                if not joint_hmc:   # 270-277
+                if not (joint_hmc or gradient_descent_joint):   # 270-277
                     # sample_error_precision (branch_sampler.rs:190-202)
                     a, s = O.ridge_posterior_params(k_out, s_out, float(np.sum(self.residual ** 2)), n)
                     br.error_precision = d.gamma(a, s)
@@ -150,7 +152,12 @@ class NetOracle:
                 self.residual = self.residual + prev
                 target = self.residual.astype(np.float32).astype(np.float64)      # the f32 target on the device
                 f32 = lambda v: np.float64(np.float32(v))   # noqa: E731  (the device's f32 draws)
-                if joint_hmc:   # hmc_step_joint (branch_sampler.rs:1070-1178), random step sizes (654-704)
+                if gradient_descent:   # branch_sampler.rs:964-1016
+                    out = O.gradient_descent(br, self.X[b], target, factor, L_int)
+                elif gradient_descent_joint:   # 1019-1066
+                    br.out_reg_sum, br.out_num_params = others, self.g_num
+                    out = O.gradient_descent_joint(br, self.X[b], target, self.hp, factor, L_int)
+                elif joint_hmc:   # hmc_step_joint (branch_sampler.rs:1070-1178), random step sizes (654-704)
                     P, Q = br.num_params, O.precision_vec(br).size
                     f = np.float32(np.float32(P + Q) ** np.float32(-0.25)) * np.float32(factor)
                     eps = np.array([f32(np.float32(d.uniform()) * f) for _ in range(P + Q)])

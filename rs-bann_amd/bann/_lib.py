@@ -53,7 +53,8 @@ class McmcCfg(C.Structure):
                 ("hmc_integration_length", C.c_int32), ("hmc_step_size_mode", C.c_int32),
                 ("chain_length", C.c_int32), ("burn_in", C.c_int32), ("fixed_param_precisions", C.c_int32),
                 ("sampled_output_bias", C.c_int32), ("trace", C.c_int32), ("trajectories", C.c_int32),
-                ("joint_hmc", C.c_int32)]
+                ("joint_hmc", C.c_int32), ("gradient_descent", C.c_int32),
+                ("gradient_descent_joint", C.c_int32)]
 
 
 # bann_allreduce_fn: in-place sum over ranks of a host buffer (dtype 0 f32, 1 f64)
@@ -110,6 +111,9 @@ SIGNATURES = {
     "bann_rss": (C.c_int, [_P, _i32, _pf64]),
     "bann_log_density_gradient": (C.c_int, [_P, _i32, _pf32, _pf64]),
     "bann_log_density": (C.c_int, [_P, _i32, _f64, _pf64]),
+    "bann_log_density_gradient_many": (C.c_int, [_P, _pi32, _i32, _pf32, _pf64]),
+    "bann_log_density_gradient_joint": (C.c_int, [_P, _i32, _pf32, _pf32, _pf64, _pf64]),
+    "bann_forward_feed": (C.c_int, [_P, _i32, _pf32, _pf32]),
     "bann_neg_hamiltonian": (C.c_int, [_P, _i32, _pf32, _pf64]),
     "bann_hmc_step": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pi32, _pf64,
                                 _pi32, _pf64]),
@@ -163,6 +167,10 @@ SIGNATURES = {
     "bann_net_train_single_branch": (C.c_int, [_P, _pf32, _i64, C.POINTER(McmcCfg), C.c_char_p]),
     "bann_net_perturb": (C.c_int, [_P, _i32, _f32, _i32, _f32]),
     "bann_net_predict": (C.c_int, [_P, _P, _pf32]),
+    "bann_net_rss": (C.c_int, [_P, _P, _pf32, _i64, _pf64]),
+    "bann_net_gradient": (C.c_int, [_P, _P, _pf32, _i64, _pf32]),
+    "bann_net_branch_r2s": (C.c_int, [_P, _P, _pf32, _i64, _pf32]),
+    "bann_net_activations": (C.c_int, [_P, _P, _i32, _pf32]),
     "bann_net_summary": (C.c_int, [_P, C.POINTER(TrainSummary)]),
     "bann_net_records": (C.c_int, [_P, _pf32, _pf32, _i32]),
     "bann_net_residual": (C.c_int, [_P, _pf32]),
@@ -170,6 +178,8 @@ SIGNATURES = {
     "bann_net_records_test": (C.c_int, [_P, _pf32, _i32]),
     "bann_set_trajectory_recording": (C.c_int, [_P, _i32]),
     "bann_branch_get_trajectory": (C.c_int, [_P, _i32, _i32, _pi32, _pf32, _pf32, _pf64]),
+    "bann_branch_get_trajectory_joint": (C.c_int, [_P, _i32, _i32, _pi32, _pf32, _pf32, _pf32, _pf64]),
+    "bann_set_graph_replay": (C.c_int, [_P, _i32]),
     "bann_net_save": (C.c_int, [_P, C.c_char_p]),
     "bann_net_load": (C.c_int, [_P, C.c_char_p]),
     "bann_net_last_error": (C.c_char_p, [_P]),

@@ -209,6 +209,52 @@ class BannContext:
         self._check(self._lib.bann_log_density_gradient(self._h, b, _ptr(g, C.c_float), C.byref(r)))
         return g, r.value
 
+    def log_density_gradient_many(self, branches):
+        """(list of param_vec gradients, rss array) of several branches from one packed launch."""
+        bl = np.ascontiguousarray(branches, dtype=np.int32)
+        sizes = [self.num_params(int(b)) for b in bl]
+        g = np.zeros(sum(sizes), np.float32)
+        r = np.zeros(bl.size, np.float64)
+        self._check(self._lib.bann_log_density_gradient_many(self._h, _ptr(bl, C.c_int32), bl.size, _ptr(g, C.c_float),
+                                                             _ptr(r, C.c_double)))
+        return np.split(g, np.cumsum(sizes)[:-1]), r
+
+    def log_density_gradient_joint(self, b: int, hyper):
+        """(grad [P + Q], rss, joint log density) at the current params and precisions."""
+        hp = _f32(hyper)
+        if hp.size != 6:
+            raise ValueError("hyper needs 6 values")
+        g = np.zeros(self.num_params(b) + self.num_precisions(b), np.float32)
+        r, ld = C.c_double(), C.c_double()
+        self._check(self._lib.bann_log_density_gradient_joint(self._h, b, _ptr(hp, C.c_float), _ptr(g, C.c_float),
+                                                              C.byref(r), C.byref(ld)))
+        return g, r.value, ld.value
+
+    def forward_feed(self, b: int, pre: bool = True):
+        """forward_feed (branch_sampler.rs:743-782): (pre-activations, activations) as lists of
+        [n, w_l] arrays per layer (the output layer's activation last; no pre-activation for it)."""
+        _, L, widths, _, _ = self.branch_info(b)
+        n = self.n
+        act = np.zeros(sum(widths) * n, np.float32)
+        pr = np.zeros(sum(widths[:-1]) * n, np.float32) if pre else None
+        self._check(self._lib.bann_forward_feed(self._h, b, _ptr(pr, C.c_float) if pre else None,
+                                                _ptr(act, C.c_float)))
+        def split(v, ws):
+            out, o = [], 0
+            for w in ws:
+                out.append(v[o: o + w * n].reshape(w, n).T)
+                o += w * n
+            return out
+        return (split(pr, widths[:-1]) if pre else None), split(act, widths)
+
+    def branch_info(self, b: int):
+        """(markers, num_layers, layer widths, activation code, prior code) of branch b."""
+        m, L, act, pr = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        w = np.zeros(64, np.int32)
+        self._check(self._lib.bann_branch_info(self._h, b, C.byref(m), C.byref(L), _ptr(w, C.c_int32), 64,
+                                               C.byref(act), C.byref(pr)))
+        return m.value, L.value, [int(v) for v in w[: L.value]], act.value, pr.value
+
     def log_density(self, b: int, rss: float) -> float:
         out = C.c_double()
         self._check(self._lib.bann_log_density(self._h, b, float(rss), C.byref(out)))
@@ -269,6 +315,25 @@ class BannContext:
         self._check(self._lib.bann_branch_get_trajectory(self._h, b, k, C.byref(steps), _ptr(pr, C.c_float),
                                                          _ptr(lg, C.c_float), _ptr(h, C.c_double)))
         return dict(params=pr, ldg=lg, hamiltonian=h)
+
+    def get_trajectory_joint(self, b: int):
+        """last recorded joint trajectory of branch b: dict(params [steps, P], precisions [steps, Q],
+        ldg [steps, P + Q], hamiltonian [steps+1])."""
+        steps = C.c_int32()
+        self._check(self._lib.bann_branch_get_trajectory_joint(self._h, b, 0, C.byref(steps), None, None, None, None))
+        k, P, Q = steps.value, self.num_params(b), self.num_precisions(b)
+        pr = np.zeros((k, P), np.float32)
+        pq = np.zeros((k, Q), np.float32)
+        lg = np.zeros((k, P + Q), np.float32)
+        h = np.zeros(k + 1, np.float64)
+        self._check(self._lib.bann_branch_get_trajectory_joint(self._h, b, k, C.byref(steps), _ptr(pr, C.c_float),
+                                                               _ptr(pq, C.c_float), _ptr(lg, C.c_float),
+                                                               _ptr(h, C.c_double)))
+        return dict(params=pr, precisions=pq, ldg=lg, hamiltonian=h)
+
+    def set_graph_replay(self, enabled: bool):
+        """bann_hmc_step: replay each trajectory's launch sequence as one captured HIP graph."""
+        self._check(self._lib.bann_set_graph_replay(self._h, 1 if enabled else 0))
 
     def set_output_stats(self, b: int, reg_sum_others: float, num_params: float):
         """OutputWeightSummaryStats of branch b for the joint density (params.rs:404-465)."""

@@ -37,13 +37,16 @@ class MCMCConfig:
     trace: bool = False          # outdir/trace: BranchCfgs as JSON per sweep (net.rs:241-244, 350-353)
     trajectories: bool = False   # outdir/traj: one Trajectory JSON per HMC step (trajectory.rs)
     joint_hmc: bool = False      # hmc_step_joint over params and precisions, no Gibbs draws (net.rs:270-290)
+    gradient_descent: bool = False        # BranchSampler::gradient_descent (line search, branch_sampler.rs:964-1016)
+    gradient_descent_joint: bool = False  # gradient_descent_joint (params and precisions, 1019-1066)
 
     def to_c(self) -> McmcCfg:
         burn = self.chain_length - 1 if self.burn_in is None else self.burn_in
         return McmcCfg(self.hmc_step_size_factor, self.hmc_max_hamiltonian_error, self.hmc_integration_length,
                        STEP_MODES[self.hmc_step_size_mode], self.chain_length, max(burn, 0),
                        int(self.fixed_param_precisions), int(self.sampled_output_bias), int(self.trace),
-                       int(self.trajectories), int(self.joint_hmc))
+                       int(self.trajectories), int(self.joint_hmc), int(self.gradient_descent),
+                       int(self.gradient_descent_joint))
 
 
 class Net:
@@ -115,6 +118,53 @@ class Net:
         self._check(self._lib.bann_net_predict(self._h, c._h if ctx is not None else None,
                                                out.ctypes.data_as(C.POINTER(C.c_float))))
         return out
+
+    def _ctxh(self, ctx):
+        return ctx._h if ctx is not None else None
+
+    def rss(self, y, ctx=None) -> float:
+        """Net::rss (net.rs:637-642): sum (y - predict)^2 on ctx's cohort (default: training)."""
+        v = np.ascontiguousarray(y, dtype=np.float32)
+        r = C.c_double()
+        self._check(self._lib.bann_net_rss(self._h, self._ctxh(ctx), v.ctypes.data_as(C.POINTER(C.c_float)), v.size,
+                                           C.byref(r)))
+        return r.value
+
+    def mse(self, y, ctx=None) -> float:
+        """Net::mse (net.rs:644-646)."""
+        return self.rss(y, ctx) / np.asarray(y).size
+
+    def gradient(self, y, ctx=None):
+        """Net::gradient (net.rs:520-527): per branch the log-density gradient against y (param_vec order)."""
+        c = ctx if ctx is not None else self._ctx
+        v = np.ascontiguousarray(y, dtype=np.float32)
+        sizes = [c.num_params(b) for b in range(c.num_branches)]
+        out = np.zeros(sum(sizes), np.float32)
+        self._check(self._lib.bann_net_gradient(self._h, self._ctxh(ctx), v.ctypes.data_as(C.POINTER(C.c_float)),
+                                                v.size, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return np.split(out, np.cumsum(sizes)[:-1])
+
+    def branch_r2s(self, y, ctx=None) -> np.ndarray:
+        """Net::branch_r2s (net.rs:648-656): 1 - rss_b / sum y^2 per branch."""
+        c = ctx if ctx is not None else self._ctx
+        v = np.ascontiguousarray(y, dtype=np.float32)
+        out = np.zeros(c.num_branches, np.float32)
+        self._check(self._lib.bann_net_branch_r2s(self._h, self._ctxh(ctx), v.ctypes.data_as(C.POINTER(C.c_float)),
+                                                  v.size, out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
+
+    def activations(self, b: int, ctx=None):
+        """Net::activations (net.rs:509-518) of branch b: per layer an [n, w_l] array."""
+        c = ctx if ctx is not None else self._ctx
+        _, L, widths, _, _ = c.branch_info(b)
+        out = np.zeros(sum(widths) * c.n, np.float32)
+        self._check(self._lib.bann_net_activations(self._h, self._ctxh(ctx), b,
+                                                   out.ctypes.data_as(C.POINTER(C.c_float))))
+        res, o = [], 0
+        for w in widths:
+            res.append(out[o: o + w * c.n].reshape(w, c.n).T)
+            o += w * c.n
+        return res
 
     def summary(self) -> dict:
         s = TrainSummary()

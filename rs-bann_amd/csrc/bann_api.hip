@@ -693,6 +693,11 @@ extern "C" int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled) {
   ctx->fused_enabled = enabled != 0;
   return BANN_OK;
 }
+extern "C" int bann_set_graph_replay(bann_ctx* ctx, int32_t enabled) {
+  if (!ctx) return BANN_E_ARG;
+  ctx->graph_replay = enabled != 0;
+  return BANN_OK;
+}
 extern "C" int64_t bann_packed_genotype_bytes(const bann_ctx* ctx) { return ctx ? ctx->packed_bytes : 0; }
 
 extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
@@ -1164,6 +1169,103 @@ extern "C" int bann_log_density_gradient(bann_ctx* ctx, int32_t b, float* grad_o
   return BANN_OK;
 }
 
+// Net::gradient (net.rs:520-527): the log-density gradients of several branches
+// against their current targets from one packed gradient launch
+extern "C" int bann_log_density_gradient_many(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* grad_out,
+                                              double* rss_out) {
+  if (!ctx || !branches || nb <= 0 || !grad_out) return fail(ctx, BANN_E_ARG, "bad branch list or null output");
+  if (!ctx->finalized) return fail(ctx, BANN_E_STATE, "call bann_finalize first");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  for (int i = 0; i < nb; ++i) {
+    if (!check_branch(ctx, branches[i])) return fail(ctx, BANN_E_ARG, "bad branch");
+    for (int k = 0; k < i; ++k)
+      if (branches[i] == branches[k]) return fail(ctx, BANN_E_ARG, "duplicate branch in list");
+  }
+  Plan p;
+  int rc = build_plan(ctx, branches, nb, p, false);
+  if (rc) return rc;
+  rc = run_grad(ctx, p, 0);
+  if (rc) return rc;
+  run_update(ctx, p, MODE_GRAD, 0);
+  CK(hipGetLastError());
+  int64_t off = 0;
+  for (int i = 0; i < nb; ++i) {
+    const BranchHost& h = ctx->br[branches[i]];
+    CK(hipMemcpyAsync(grad_out + off, ctx->d_grad + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost,
+                      ctx->stream));
+    if (rss_out) CK(hipMemcpyAsync(rss_out + i, ctx->d_rss + branches[i], sizeof(double), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    off += h.P;
+  }
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+// log_density_gradient_joint (branch_sampler.rs:406-422) at the branch's current
+// parameters and precisions: [params | precisions], the joint log density
+// (log_density_joint 292-305) and the rss; k_update_joint in MODE_GRAD
+extern "C" int bann_log_density_gradient_joint(bann_ctx* ctx, int32_t b, const float* hyper, float* grad_out,
+                                               double* rss_out, double* log_density_out) {
+  if (!check_branch(ctx, b) || !hyper || !grad_out) return fail(ctx, BANN_E_ARG, "bad branch or null pointer");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  const BranchHost& h = ctx->br[b];
+  if (h.prior == BANN_STD_NORMAL)
+    return fail(ctx, BANN_E_ARG, "std_normal has no joint density (std_normal_branch.rs:119-131)");
+  if (h.dev.nq > BANN_JOINT_MAXQ) return fail(ctx, BANN_E_SHAPE, "too many precisions for the joint update");
+  for (int k = 0; k < 6; ++k) ctx->st.hyper[k] = hyper[k];
+  const float ows[2] = {h.ows_reg_sum, h.ows_num >= 0.f ? h.ows_num : (float)h.widths[h.L - 2]};
+  CK(hipMemcpyAsync(ctx->d_phi + h.dev.q_off, h.prec.data(), h.dev.nq * sizeof(float), hipMemcpyHostToDevice,
+                    ctx->stream));
+  CK(hipMemcpyAsync(ctx->d_ows + 2 * b, ows, 2 * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  Plan p;
+  int rc = build_plan(ctx, &b, 1, p, false);
+  if (rc) return rc;
+  rc = run_grad(ctx, p, 0);
+  if (rc) return rc;
+  launch_update_joint(ctx->st, p.d_all, 1, MODE_GRAD, 0, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(grad_out, ctx->d_grad + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(grad_out + h.P, ctx->d_gphi + h.dev.q_off, h.dev.nq * sizeof(float), hipMemcpyDeviceToHost,
+                    ctx->stream));
+  double r[2] = {0.0, 0.0};
+  CK(hipMemcpyAsync(&r[0], ctx->d_rss + b, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(&r[1], ctx->d_ld + b, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  if (rss_out) *rss_out = r[0];
+  if (log_density_out) *log_density_out = r[1];
+  return BANN_OK;
+}
+
+// forward_feed (branch_sampler.rs:743-782) with every layer kept, for
+// Net::activations (net.rs:509-518): kernels_feed.hip, scratch per call
+extern "C" int bann_forward_feed(bann_ctx* ctx, int32_t b, float* pre_out, float* act_out) {
+  if (!check_branch(ctx, b) || !act_out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  const BranchHost& h = ctx->br[b];
+  int64_t wa = 0, wp = 0;
+  for (int l = 0; l < h.L; ++l) {
+    wa += h.widths[l];
+    if (l < h.L - 1) wp += h.widths[l];
+  }
+  const int64_t n = ctx->n;
+  float *d_act = nullptr, *d_pre = nullptr;
+  CK(dalloc(&d_act, wa * n));
+  if (pre_out && dalloc(&d_pre, wp * n) != hipSuccess) {
+    dfree(d_act);
+    return fail(ctx, BANN_E_OOM, "forward_feed scratch");
+  }
+  launch_forward_feed(ctx->st, b, h.dev, d_pre, d_act, ctx->stream);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpyAsync(act_out, d_act, wa * n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && pre_out)
+    e = hipMemcpyAsync(pre_out, d_pre, wp * n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  dfree(d_act);
+  dfree(d_pre);
+  CK(e);
+  return BANN_OK;
+}
+
 // host evaluation of log_density at the current parameters (branch_sampler.rs:72-78)
 static int host_log_density(bann_ctx* ctx, int32_t b, double rss, double* out) {
   const BranchHost& h = ctx->br[b];
@@ -1331,6 +1433,24 @@ static int traj_launches(bann_ctx* ctx, const Plan& p, int32_t L) {
   return BANN_OK;
 }
 
+// trajectory recording: the -H trace of every recorded branch after the stream
+// has drained; an early rejection leaves the later entries unwritten (NaN) and
+// ends the recorded steps there (branch_sampler.rs:1264-1279)
+static int rec_finish(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L) {
+  const int stride = ctx->htrace_cap;
+  for (int i = 0; i < nb; ++i) {
+    auto& R = ctx->rec[branches[i]];
+    R.h.assign(L + 1, 0.0);
+    CK(hipMemcpy(R.h.data(), ctx->d_htrace + (int64_t)branches[i] * stride, (L + 1) * sizeof(double),
+                 hipMemcpyDeviceToHost));
+    int steps = 0;
+    while (steps < L && R.h[steps + 1] == R.h[steps + 1]) ++steps;
+    R.steps = steps;
+    R.h.resize(steps + 1);
+  }
+  return BANN_OK;
+}
+
 static int traj_replay(bann_ctx* ctx, const Plan& p, int32_t L) {
   const std::string key = traj_graph_key(ctx, p, L);
   hipGraphExec_t exec = nullptr;
@@ -1398,6 +1518,8 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
     ctx->rec.resize(ctx->br.size());
     for (int i = 0; i < nb; ++i) {
       auto& R = ctx->rec[branches[i]];
+      R.q = 0;
+      R.prec.clear();
       R.params.assign((size_t)L * ctx->br[branches[i]].P, 0.f);
       R.ldg.assign((size_t)L * ctx->br[branches[i]].P, 0.f);
     }
@@ -1424,18 +1546,10 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   mark_predictions(ctx, p, true);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
-  const int stride = ctx->htrace_cap;
-  if (ctx->rec_on)
-    for (int i = 0; i < nb; ++i) {  // -H trace; an early rejection leaves the later entries unwritten (NaN)
-      auto& R = ctx->rec[branches[i]];
-      R.h.assign(L + 1, 0.0);
-      CK(hipMemcpy(R.h.data(), ctx->d_htrace + (int64_t)branches[i] * stride, (L + 1) * sizeof(double),
-                   hipMemcpyDeviceToHost));
-      int steps = 0;
-      while (steps < L && R.h[steps + 1] == R.h[steps + 1]) ++steps;
-      R.steps = steps;
-      R.h.resize(steps + 1);
-    }
+  if (ctx->rec_on) {
+    const int rc2 = rec_finish(ctx, branches, nb, L);
+    if (rc2) return rc2;
+  }
   return hmc_outputs(ctx, branches, nb, L, status_out, h_trace_out, uturn_out, log_density_out);
 }
 
@@ -1503,18 +1617,52 @@ extern "C" int bann_hmc_step_joint(bann_ctx* ctx, const int32_t* branches, int32
     launch_sample_momentum_joint(ctx->st, p.d_all, nb, max_q, seed, ctx->stream);
   }
   CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
+  mark_predictions(ctx, p, false);  // theta moves (launch_update_joint does not go through run_update)
+  if (ctx->rec_on) {  // the joint Trajectory (1126-1135): params, precisions, joint ldg [params | precisions], -H
+    ctx->rec.resize(ctx->br.size());
+    for (int i = 0; i < nb; ++i) {
+      auto& R = ctx->rec[branches[i]];
+      const BranchHost& h = ctx->br[branches[i]];
+      R.q = h.dev.nq;
+      R.params.assign((size_t)L * h.P, 0.f);
+      R.prec.assign((size_t)L * R.q, 0.f);
+      R.ldg.assign((size_t)L * (h.P + R.q), 0.f);
+    }
+  }
   rc = run_grad(ctx, p, 2);  // f(theta_0) -> pred0
   if (rc) return rc;
   launch_update_joint(ctx->st, p.d_all, nb, MODE_INIT, 0, ctx->stream);
   for (int k = 1; k <= L; ++k) {
     rc = run_grad(ctx, p, k == L ? 1 : 0);
     if (rc) return rc;
+    if (ctx->rec_on)  // (theta_k, phi_k) after the k-th position step
+      for (int i = 0; i < nb; ++i) {
+        const BranchHost& h = ctx->br[branches[i]];
+        auto& R = ctx->rec[branches[i]];
+        CK(hipMemcpyAsync(R.params.data() + (size_t)(k - 1) * h.P, ctx->d_theta + h.dev.p_off, h.P * sizeof(float),
+                          hipMemcpyDeviceToHost, ctx->stream));
+        CK(hipMemcpyAsync(R.prec.data() + (size_t)(k - 1) * R.q, ctx->d_phi + h.dev.q_off, R.q * sizeof(float),
+                          hipMemcpyDeviceToHost, ctx->stream));
+      }
     launch_update_joint(ctx->st, p.d_all, nb, k < L ? MODE_STEP : MODE_LAST, k, ctx->stream);
+    if (ctx->rec_on)  // the joint log-density gradient there
+      for (int i = 0; i < nb; ++i) {
+        const BranchHost& h = ctx->br[branches[i]];
+        auto& R = ctx->rec[branches[i]];
+        float* row = R.ldg.data() + (size_t)(k - 1) * (h.P + R.q);
+        CK(hipMemcpyAsync(row, ctx->d_grad + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+        CK(hipMemcpyAsync(row + h.P, ctx->d_gphi + h.dev.q_off, R.q * sizeof(float), hipMemcpyDeviceToHost,
+                          ctx->stream));
+      }
   }
   launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);  // rejected: predictions back to f(theta_0)
   mark_predictions(ctx, p, true);
   CK(hipGetLastError());
   CK(hipStreamSynchronize(ctx->stream));
+  if (ctx->rec_on) {
+    rc = rec_finish(ctx, branches, nb, L);
+    if (rc) return rc;
+  }
   const int stride = ctx->htrace_cap;
   for (int i = 0; i < nb; ++i) {
     const int b = branches[i];
@@ -1543,11 +1691,28 @@ extern "C" int bann_branch_get_trajectory(bann_ctx* ctx, int32_t b, int32_t cap,
   if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
   if (b >= (int32_t)ctx->rec.size() || ctx->rec[b].h.empty()) return fail(ctx, BANN_E_STATE, "no recorded trajectory");
   const auto& R = ctx->rec[b];
+  if (R.q) return fail(ctx, BANN_E_STATE, "the last recorded trajectory is joint (bann_branch_get_trajectory_joint)");
   const int64_t P = ctx->br[b].P;
   const int32_t k = std::min(cap, R.steps);
   if (steps) *steps = R.steps;
   if (params) std::copy(R.params.begin(), R.params.begin() + k * P, params);
   if (ldg) std::copy(R.ldg.begin(), R.ldg.begin() + k * P, ldg);
+  if (hamiltonian) std::copy(R.h.begin(), R.h.begin() + k + 1, hamiltonian);
+  return BANN_OK;
+}
+
+extern "C" int bann_branch_get_trajectory_joint(bann_ctx* ctx, int32_t b, int32_t cap, int32_t* steps, float* params,
+                                                float* precisions, float* ldg, double* hamiltonian) {
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  if (b >= (int32_t)ctx->rec.size() || ctx->rec[b].h.empty()) return fail(ctx, BANN_E_STATE, "no recorded trajectory");
+  const auto& R = ctx->rec[b];
+  if (!R.q) return fail(ctx, BANN_E_STATE, "the last recorded trajectory is not joint (bann_branch_get_trajectory)");
+  const int64_t P = ctx->br[b].P, Q = R.q;
+  const int32_t k = std::min(cap, R.steps);
+  if (steps) *steps = R.steps;
+  if (params) std::copy(R.params.begin(), R.params.begin() + k * P, params);
+  if (precisions) std::copy(R.prec.begin(), R.prec.begin() + k * Q, precisions);
+  if (ldg) std::copy(R.ldg.begin(), R.ldg.begin() + k * (P + Q), ldg);
   if (hamiltonian) std::copy(R.h.begin(), R.h.begin() + k + 1, hamiltonian);
   return BANN_OK;
 }

@@ -203,5 +203,7 @@ void launch_step_sizes(const DevState& st, const double* base, const int32_t* br
 void launch_restore_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);
 int64_t residual_delta_scratch_floats(int64_t n);
+// forward_feed with every layer (kernels_feed.hip): pre [sum_{l<L-1} w_l][n] (may be null), act [sum_l w_l][n]
+void launch_forward_feed(const DevState& st, int b, const BranchDev& bd, float* pre, float* act, hipStream_t s);
 void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* scratch, float* out,
                            hipStream_t s);

@@ -409,23 +409,35 @@ std::string trace_line(const bann_net* t) {
 }
 
 // one Trajectory (trajectory.rs:3-11) of the last hmc_step of branch b as serde_json
-int traj_line(bann_net* t, int b, std::string& o) {
+// one Trajectory JSON line (trajectory.rs:1-43): hmc_step records params, ldg and
+// -H (branch_sampler.rs:1253-1289), hmc_step_joint also the precisions and the
+// joint ldg [params | precisions] (1126-1135)
+int traj_line(bann_net* t, int b, bool joint, std::string& o) {
   const Branch& B = t->br[b];
+  const int64_t Q = joint ? B.NP : 0, G = B.P + Q;
   int32_t steps = 0;
-  CKB(bann_branch_get_trajectory(t->ctx, b, 0, &steps, nullptr, nullptr, nullptr));
-  std::vector<float> pr((size_t)steps * B.P), lg((size_t)steps * B.P);
+  if (joint)
+    CKB(bann_branch_get_trajectory_joint(t->ctx, b, 0, &steps, nullptr, nullptr, nullptr, nullptr));
+  else
+    CKB(bann_branch_get_trajectory(t->ctx, b, 0, &steps, nullptr, nullptr, nullptr));
+  std::vector<float> pr((size_t)steps * B.P), pq((size_t)steps * Q), lg((size_t)steps * G);
   std::vector<double> h(steps + 1);
-  CKB(bann_branch_get_trajectory(t->ctx, b, steps, &steps, pr.data(), lg.data(), h.data()));
+  if (joint)
+    CKB(bann_branch_get_trajectory_joint(t->ctx, b, steps, &steps, pr.data(), pq.data(), lg.data(), h.data()));
+  else
+    CKB(bann_branch_get_trajectory(t->ctx, b, steps, &steps, pr.data(), lg.data(), h.data()));
+  auto rows = [&](const std::vector<float>& v, int64_t w) {
+    for (int k = 0; k < steps; ++k) {
+      if (k) o += ',';
+      jvec(o, v.data() + (size_t)k * w, w);
+    }
+  };
   o = "{\"params\":[";
-  for (int k = 0; k < steps; ++k) {
-    if (k) o += ',';
-    jvec(o, pr.data() + (size_t)k * B.P, B.P);
-  }
-  o += "],\"precisions\":[],\"ldg\":[";
-  for (int k = 0; k < steps; ++k) {
-    if (k) o += ',';
-    jvec(o, lg.data() + (size_t)k * B.P, B.P);
-  }
+  rows(pr, B.P);
+  o += "],\"precisions\":[";
+  if (joint) rows(pq, Q);
+  o += "],\"ldg\":[";
+  rows(lg, G);
   o += "],\"num_ldg\":[],\"hamiltonian\":[";
   for (int k = 0; k <= steps; ++k) {
     if (k) o += ',';
@@ -649,6 +661,85 @@ struct Draws {
   float u = 0.f;
 };
 
+// BranchParams::descend_gradient (params.rs:740-749; 357-367 for the precisions):
+// v += step * g in f32, the ArrayFire op order (the product rounds first)
+void descend(std::vector<float>& v, const float* g, float step) {
+  for (size_t i = 0; i < v.size(); ++i) {
+    const float d = step * g[i];
+    v[i] = v[i] + d;
+  }
+}
+
+// BranchSampler::gradient_descent (branch_sampler.rs:964-1002): L ascent steps
+// on the log density, each with a doubling / halving line search over rss
+// probes (probe_gradient_step, 1004-1016); always Accepted.  Every probe and
+// gradient runs on the device (bann_rss / bann_log_density_gradient); the
+// parameter vector moves on the host, in f32 as the reference.
+int gradient_descent(bann_net* t, int b, const bann_mcmc_cfg* cfg, int32_t& status) {
+  Branch& B = t->br[b];
+  std::vector<float> th(B.P), g(B.P), probe(B.P);
+  CKB(bann_branch_get_params(t->ctx, b, th.data()));
+  CKB(bann_log_density_gradient(t->ctx, b, g.data(), nullptr));
+  auto probe_rss = [&](float step, double& r) -> int {
+    probe = th;
+    descend(probe, g.data(), step);
+    CKB(bann_branch_set_params(t->ctx, b, probe.data()));
+    CKB(bann_rss(t->ctx, b, &r));
+    return BANN_OK;
+  };
+  for (int k = 0; k < cfg->hmc_integration_length; ++k) {
+    float step = cfg->hmc_step_size_factor;
+    double prev = 0.0, twice = 0.0, curr = 0.0;
+    int rc = probe_rss(step, prev);
+    if (!rc) rc = probe_rss(2.f * step, twice);
+    if (rc) return rc;
+    const float f = twice < prev ? 2.f : 0.5f;
+    step *= f;
+    if ((rc = probe_rss(step, curr))) return rc;
+    // terminates: halving reaches step * g == 0 (rss == prev), doubling inf / NaN
+    for (int guard = 0; curr < prev && guard < 4096; ++guard) {
+      prev = curr;
+      step *= f;
+      if ((rc = probe_rss(step, curr))) return rc;
+    }
+    step /= f;
+    descend(th, g.data(), step);
+    CKB(bann_branch_set_params(t->ctx, b, th.data()));
+    CKB(bann_log_density_gradient(t->ctx, b, g.data(), nullptr));
+  }
+  status = BANN_ACCEPTED;
+  return BANN_OK;
+}
+
+// BranchSampler::gradient_descent_joint (branch_sampler.rs:1019-1066): L ascent
+// steps of the parameters and the precisions along the joint log-density
+// gradient at the fixed step size factor; Rejected (state restored) if the error
+// precision ends <= 0, else Accepted.
+int gradient_descent_joint(bann_net* t, int b, const bann_mcmc_cfg* cfg, double others, int32_t& status) {
+  Branch& B = t->br[b];
+  const float hyper[6] = {t->hp.dense_shape, t->hp.dense_scale, t->hp.summary_shape,
+                          t->hp.summary_scale, t->hp.output_shape, t->hp.output_scale};
+  CKB(bann_branch_set_output_stats(t->ctx, b, (float)others, (float)t->g_num));
+  std::vector<float> th(B.P), pr = B.prec, g(B.P + B.NP);
+  CKB(bann_branch_get_params(t->ctx, b, th.data()));
+  const std::vector<float> th0 = th, pr0 = pr;
+  CKB(bann_log_density_gradient_joint(t->ctx, b, hyper, g.data(), nullptr, nullptr));
+  for (int k = 0; k < cfg->hmc_integration_length; ++k) {
+    descend(th, g.data(), cfg->hmc_step_size_factor);
+    descend(pr, g.data() + B.P, cfg->hmc_step_size_factor);
+    CKB(bann_branch_set_params(t->ctx, b, th.data()));
+    CKB(bann_branch_set_precisions(t->ctx, b, pr.data()));
+    CKB(bann_log_density_gradient_joint(t->ctx, b, hyper, g.data(), nullptr, nullptr));
+  }
+  status = BANN_ACCEPTED;
+  if (!(pr[B.epoff] > 0.f)) {  // scalar_to_host(error_precision) <= 0.0 (1058-1062)
+    CKB(bann_branch_set_params(t->ctx, b, th0.data()));
+    CKB(bann_branch_set_precisions(t->ctx, b, pr0.data()));
+    status = BANN_REJECTED;
+  }
+  return BANN_OK;
+}
+
 // one branch update of Net::train / train_single_branch (net.rs:261-332): Gibbs
 // draws (unless joint), target = residual + f_b, the HMC trajectory on the
 // device, the residual bookkeeping on the device, global params, output bias
@@ -656,10 +747,18 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   Branch& B = t->br[b];
   const int64_t n = t->n;
   const double kout = t->hp.output_shape, sout = t->hp.output_scale;
+  // cfg.update_global_params (net.rs:261-262).  train_single_branch applies it
+  // AFTER from_cfg (net.rs:416-418), i.e. the branch runs on its cfg's values --
+  // which are the globals too: initialize_stats (net.rs:158-166) applied them to
+  // every cfg before the first iteration, and every later cfg is to_cfg of the
+  // branch whose values became the globals (update_from_branch_cfg, 447-449)
   cfg_update_global(t, B);
   const double others = B.ows_reg_sum - B.out_stat();  // from_cfg (branch_struct.rs:26)
-  const bool joint = cfg->joint_hmc != 0;
-  if (!joint) {  // net.rs:270-277
+  // net.rs:270-277: no Gibbs draws for the joint samplers; the step (282-290):
+  // gradient descent, joint gradient descent, joint HMC, else HMC
+  const bool gd = cfg->gradient_descent != 0, gdj = !gd && cfg->gradient_descent_joint != 0;
+  const bool joint = cfg->joint_hmc != 0 && !gd && !gdj;
+  if (!(cfg->gradient_descent_joint || cfg->joint_hmc)) {
     // sample_error_precision (branch_sampler.rs:190-202): output-layer hyperparameters
     B.prec[B.epoff] = (float)ridge_posterior(t, kout, sout, t->rss_cur, (double)n);
     if (!cfg->fixed_param_precisions) {  // sample_param_precisions (173-188)
@@ -672,7 +771,14 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
   CKB(bann_residual_to_target(t->ctx, b));  // net.rs:279-280: fitted to residual + its own prediction
   int32_t status = 0;
-  if (joint) {  // hmc_step_joint (branch_sampler.rs:1070-1178): random step sizes over [params | precisions]
+  if (gd) {
+    int rc = gradient_descent(t, b, cfg, status);
+    if (rc) return rc;
+  } else if (gdj) {
+    int rc = gradient_descent_joint(t, b, cfg, others, status);
+    if (rc) return rc;
+    CKB(bann_branch_get_precisions(t->ctx, b, B.prec.data()));  // to_cfg
+  } else if (joint) {  // hmc_step_joint (branch_sampler.rs:1070-1178): random step sizes over [params | precisions]
     const int64_t PQ = B.P + B.NP;
     const float f = std::pow((float)PQ, -0.25f) * cfg->hmc_step_size_factor;  // random_step_sizes (654-662)
     dr.eps.resize(PQ);
@@ -703,9 +809,9 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
     CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
                       cfg->hmc_step_size_factor, eps, dr.mom.data(), 0, &dr.u, &status, nullptr, nullptr, nullptr));
   }
-  if (traj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
+  if (traj && !gd && !gdj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
     std::string line;
-    int rc = traj_line(t, b, line);
+    int rc = traj_line(t, b, joint, line);
     if (!rc) rc = append_text(t, dir + "/traj", line);
     if (rc) return rc;
   }
@@ -872,6 +978,88 @@ extern "C" int bann_net_predict(bann_net* t, bann_ctx* ctx, float* y_hat) {
     y_hat[i] = v;
   }
   return BANN_OK;
+}
+
+namespace {
+// B::from_cfg on another context (or the net's own): the context must hold the
+// net's branches; its parameters (another context only) and precisions are
+// loaded from the BranchCfgs
+int load_cfgs(bann_net* t, bann_ctx* c, int64_t n) {
+  const int nb = (int)t->br.size();
+  if (bann_num_branches(c) != nb) return fail(t, BANN_E_SHAPE, "context branch count differs from the net");
+  if (n != bann_ctx_num_individuals(c)) return fail(t, BANN_E_SHAPE, "y length differs from the context's cohort");
+  for (int b = 0; b < nb; ++b) {
+    int32_t m = 0, L = 0, w[BANN_NET_MAXL] = {0};
+    if (bann_branch_info(c, b, &m, &L, w, BANN_NET_MAXL, nullptr, nullptr) != BANN_OK || m != t->br[b].m ||
+        L != t->br[b].L || L > BANN_NET_MAXL || !std::equal(w, w + L, t->br[b].widths.begin()))
+      return fail(t, BANN_E_SHAPE, "context branches differ from the net's");
+    int rc = c != t->ctx ? bann_branch_set_params(c, b, t->br[b].params.data()) : BANN_OK;
+    if (!rc) rc = bann_branch_set_precisions(c, b, t->br[b].prec.data());
+    if (rc < 0) return fail(t, rc, std::string("loading the branch cfgs: ") + bann_last_error(c));
+  }
+  return BANN_OK;
+}
+}  // namespace
+
+extern "C" int bann_net_rss(bann_net* t, bann_ctx* ctx, const float* y, int64_t n, double* rss_out) {
+  if (!t || !y || !rss_out) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  if (n != bann_ctx_num_individuals(c)) return fail(t, BANN_E_SHAPE, "y length differs from the context's cohort");
+  std::vector<float> yh(n);
+  const int rc = bann_net_predict(t, ctx, yh.data());
+  if (rc) return rc;
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) {  // residual = y - y_hat (f32), sum_of_squares
+    const float r = y[i] - yh[i];
+    s += (double)r * r;
+  }
+  *rss_out = s;
+  return BANN_OK;
+}
+
+extern "C" int bann_net_gradient(bann_net* t, bann_ctx* ctx, const float* y, int64_t n, float* grad_out) {
+  if (!t || !y || !grad_out) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  int rc = load_cfgs(t, c, n);
+  if (rc) return rc;
+  const int nb = (int)t->br.size();
+  std::vector<int32_t> all(nb);
+  for (int b = 0; b < nb; ++b) all[b] = b;
+  rc = bann_set_target_all(c, y);
+  if (!rc) rc = bann_log_density_gradient_many(c, all.data(), nb, grad_out, nullptr);
+  return rc < 0 ? fail(t, rc, std::string("gradient: ") + bann_last_error(c)) : BANN_OK;
+}
+
+extern "C" int bann_net_branch_r2s(bann_net* t, bann_ctx* ctx, const float* y, int64_t n, float* r2_out) {
+  if (!t || !y || !r2_out) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  int rc = load_cfgs(t, c, n);
+  if (rc) return rc;
+  const int nb = (int)t->br.size();
+  std::vector<int32_t> all(nb);
+  int64_t ptot = 0;
+  for (int b = 0; b < nb; ++b) {
+    all[b] = b;
+    ptot += t->br[b].P;
+  }
+  std::vector<float> g(ptot);
+  std::vector<double> rss(nb);
+  rc = bann_set_target_all(c, y);
+  if (!rc) rc = bann_log_density_gradient_many(c, all.data(), nb, g.data(), rss.data());
+  if (rc < 0) return fail(t, rc, std::string("branch_r2s: ") + bann_last_error(c));
+  double yy = 0.0;
+  for (int64_t i = 0; i < n; ++i) yy += (double)y[i] * y[i];
+  for (int b = 0; b < nb; ++b) r2_out[b] = 1.f - (float)rss[b] / (float)yy;  // r2 (branch_sampler.rs:911-913)
+  return BANN_OK;
+}
+
+extern "C" int bann_net_activations(bann_net* t, bann_ctx* ctx, int32_t b, float* act_out) {
+  if (!t || !act_out || b < 0 || b >= (int)t->br.size()) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  int rc = load_cfgs(t, c, bann_ctx_num_individuals(c));
+  if (rc) return rc;
+  rc = bann_forward_feed(c, b, nullptr, act_out);
+  return rc < 0 ? fail(t, rc, std::string("activations: ") + bann_last_error(c)) : BANN_OK;
 }
 
 extern "C" int bann_net_set_test_data(bann_net* t, bann_ctx* test_ctx, const float* y_test, int64_t n_test) {

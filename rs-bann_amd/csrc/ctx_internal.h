@@ -141,7 +141,9 @@ struct bann_ctx {
   bool rec_on = false;
   struct Rec {
     int32_t steps = 0;
-    std::vector<float> params, ldg;  // [L][P]
+    int32_t q = 0;                   // joint trajectory: precisions per step (0: parameters only)
+    std::vector<float> params, ldg;  // [L][P], [L][P + q]
+    std::vector<float> prec;         // [L][q]
     std::vector<double> h;           // [L + 1]
   };
   std::vector<Rec> rec;  // indexed by branch

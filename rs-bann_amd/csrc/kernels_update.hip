@@ -995,7 +995,7 @@ __global__ void __launch_bounds__(UPD_J) k_update_joint(DevState st, const int32
     const float gr = -(le * d + reg);
     st.grad[base + i] = gr;
     float p = st.mom[base + i];
-    if (mode != MODE_INIT) {  // second half step of this leapfrog step (momentum.rs:30-63)
+    if (mode == MODE_STEP || mode == MODE_LAST) {  // second half step of this leapfrog step (momentum.rs:30-63)
       p = p + st.eps[base + i] * 0.5f * gr;
       st.mom[base + i] = p;
     }
@@ -1051,7 +1051,7 @@ __global__ void __launch_bounds__(UPD_J) k_update_joint(DevState st, const int32
     const float gq = (float)g;
     st.gphi[qb + q] = gq;
     float p = st.mphi[qb + q];
-    if (mode != MODE_INIT) {
+    if (mode == MODE_STEP || mode == MODE_LAST) {
       p = p + st.ephi[qb + q] * 0.5f * gq;
       st.mphi[qb + q] = p;
     }
@@ -1063,6 +1063,13 @@ __global__ void __launch_bounds__(UPD_J) k_update_joint(DevState st, const int32
   const double ldj = sums[0];
   const double ldn = sums[2] - (double)le * rss / 2.0;
   const double h = ldj - 0.5 * sums[1];
+  if (mode == MODE_GRAD) {  // bann_log_density_gradient_joint: gradients, joint log density and rss only
+    if (t == 0) {
+      st.ld_out[b] = ldj;
+      st.rss_out[b] = rss;
+    }
+    return;
+  }
   const int stride = st.lint + 1;
   int act = 0;  // 0: (half step +) position step, 1: restore theta0 / phi0, 2: keep
   if (mode == MODE_INIT) {

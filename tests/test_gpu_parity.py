@@ -824,6 +824,7 @@ def test_hmc_step_joint_parity(Ctx, prior, shape):
     ctx.set_target(0, y)
     P, Q = br.num_params, O.precision_vec(br).size
     hp = O.Hyper(dense=HYPER[0:2], summary=HYPER[2:4], output=HYPER[4:6])
+    ctx.set_trajectory_recording(True)   # the joint Trajectory (branch_sampler.rs:1126-1135)
     for u, scale in [(0.3, 2e-4), (0.3, 3e-3), (0.5, 1.0)]:   # small, larger, absurd (early rejection)
         eps = (scale * rng.uniform(size=P + Q)).astype(np.float32)
         p0 = rng.normal(size=P + Q).astype(np.float32)
@@ -837,6 +838,17 @@ def test_hmc_step_joint_parity(Ctx, prior, shape):
         # a diverged step's -H (|dH| ~ 1e10 at scale 1) is f32 noise vs float64: check the status only there
         fin = np.isfinite(tr) & (np.abs(tr - tr[0]) <= 10.0)
         assert np.all(np.abs(gt[fin] - tr[fin]) <= 1e-5 * np.maximum(1.0, np.abs(tr[fin]))), (scale, gt, tr)
+        rec = ctx.get_trajectory_joint(0)
+        k = len(out["states"])
+        assert rec["params"].shape == (k, P) and rec["precisions"].shape == (k, Q) and rec["ldg"].shape == (k, P + Q)
+        assert np.array_equal(rec["hamiltonian"], res["trace"][0][: k + 1])
+        for j in range(k):
+            if fin[j + 1]:
+                assert norm_rel(rec["params"][j], out["states"][j][:P]) < 1e-5, (scale, j)
+                assert norm_rel(rec["precisions"][j], out["states"][j][P:]) < 1e-5, (scale, j)
+                assert norm_rel(rec["ldg"][j], out["ldgs"][j]) < 1e-5, (scale, j)
+        with pytest.raises(Exception):   # the parameter-only getter refuses a joint recording
+            ctx.get_trajectory(0)
         assert norm_rel(ctx.get_params(0), O.param_vec(ob.weights, ob.biases)) < 1e-5
         assert norm_rel(ctx.get_precisions(0), O.precision_vec(ob)) < 1e-5
         if out["status"] != O.REJECTED_EARLY:
@@ -845,6 +857,94 @@ def test_hmc_step_joint_parity(Ctx, prior, shape):
             assert np.array_equal(ctx.get_params(0), theta0)
         br = ob
     ctx.close()
+
+
+@pytest.mark.parametrize("shape", [("fx", 60, [4, 4, 1]), ("fxl", 700, [4, 3, 1]), ("wide", 40, [8, 8, 1]),
+                                   ("layered", 30, [6, 5, 3, 1]), ("layered", 90, [45, 45, 1])])
+@pytest.mark.parametrize("act", ["tanh", "relu", "silu"])
+def test_forward_feed_every_layer(Ctx, shape, act):
+    """bann_forward_feed (forward_feed, branch_sampler.rs:743-782, every layer
+    kept, for Net::activations net.rs:509-518): the pre-activations and
+    activations of every layer match the oracle on every kernel path's shapes."""
+    path, m, widths = shape
+    rng = np.random.default_rng(7)
+    n = 333
+    g = O.synthetic_genotypes(rng, n, m)
+    br = f32_branch(O.random_branch(rng, m, widths, act=act))
+    ctx = build_context(Ctx, g, [dict(snps=np.arange(m, dtype=np.int32), branch=br, y=np.zeros(n))])
+    X = oracle_inputs(ctx, g, np.arange(m))
+    pre, act_ = ctx.forward_feed(0)
+    opre, oact = O.forward_feed(br, X)
+    assert len(pre) == len(opre) == len(widths) - 1 and len(act_) == len(oact) == len(widths)
+    for a, oa in zip(pre + act_, opre + oact):
+        assert a.shape == oa.shape and norm_rel(a, oa) < 1e-5
+    ctx.close()
+
+
+def test_gradient_many_and_joint_gradient(Ctx):
+    """bann_log_density_gradient_many (one packed launch, Net::gradient) equals
+    the per-branch calls bitwise; bann_log_density_gradient_joint
+    (log_density_gradient_joint, branch_sampler.rs:406-422) and its joint log
+    density (292-305) match the oracle for ridge / lasso, ARD / base."""
+    rng = np.random.default_rng(19)
+    n = 640
+    shapes = [(60, [4, 4, 1], "ridge_ard"), (40, [8, 8, 1], "lasso_base"), (30, [6, 5, 3, 1], "lasso_ard"),
+              (700, [4, 3, 1], "ridge_base")]
+    g = O.synthetic_genotypes(rng, n, sum(m for m, _, _ in shapes))
+    specs, off = [], 0
+    for m, w, prior in shapes:
+        br = f32_branch(O.random_branch(rng, m, w, prior=prior))
+        br.out_reg_sum, br.out_num_params = float(np.float32(0.21)), 17.0
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32), branch=br,
+                          y=rng.normal(size=n).astype(np.float32)))
+        off += m
+    ctx = build_context(Ctx, g, specs)
+    grads, rss = ctx.log_density_gradient_many([3, 0, 2, 1])
+    for gv, r, b in zip(grads, rss, [3, 0, 2, 1]):
+        g1, r1 = ctx.log_density_gradient(b)
+        assert np.array_equal(gv, g1) and r == r1, b
+    hp = O.Hyper(dense=HYPER[0:2], summary=HYPER[2:4], output=HYPER[4:6])
+    for b, s in enumerate(specs):
+        br = s["branch"]
+        ctx.set_output_stats(b, br.out_reg_sum, br.out_num_params)
+        X = oracle_inputs(ctx, g, s["snps"])
+        yd = s["y"].astype(np.float64)
+        gj, r, ld = ctx.log_density_gradient_joint(b, HYPER)
+        og, orss = O.ldg_joint_vec(br, X, yd, hp)
+        P = br.num_params
+        assert norm_rel(gj[:P], og[:P]) < 1e-5 and norm_rel(gj[P:], og[P:]) < 1e-5, b
+        assert scalar_close(r, orss), b
+        old = O.log_density_joint(br, orss, hp, n)
+        assert scalar_close(ld, old), (b, ld, old)
+    ctx.close()
+
+
+def test_graph_replay_matches_launches(Ctx):
+    """bann_set_graph_replay: a trajectory replayed as one captured HIP graph
+    gives the bits of the launch-by-launch trajectory -- status, -H trace,
+    parameters and prediction rows -- over several branch sets and L (graphs are
+    keyed by plan shape, L and the kernels' by-value state)."""
+    rng = np.random.default_rng(41)
+    n = 900
+    shapes = [(60, [4, 4, 1]), (120, [4, 3, 1]), (40, [8, 8, 1]), (30, [6, 5, 3, 1])]
+    g = O.synthetic_genotypes(rng, n, sum(m for m, _ in shapes))
+    specs, off = [], 0
+    for m, w in shapes:
+        br = f32_branch(O.random_branch(rng, m, w))
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32), branch=br,
+                          y=rng.normal(size=n).astype(np.float32)))
+        off += m
+    ctxs = [build_context(Ctx, g, specs) for _ in range(2)]
+    ctxs[1].set_graph_replay(True)
+    for it, (bl, L) in enumerate([([0], 3), ([0, 1], 5), ([2], 4), ([0], 3), ([3, 1], 6), ([0, 1], 5)]):
+        out = [c.hmc_step(bl, L, 10.0, step_factor=0.3, seed=100 + it) for c in ctxs]
+        assert np.array_equal(out[0]["status"], out[1]["status"]), it
+        assert np.array_equal(out[0]["trace"], out[1]["trace"], equal_nan=True), it
+        for b in range(len(shapes)):
+            assert np.array_equal(ctxs[0].get_params(b), ctxs[1].get_params(b)), (it, b)
+            assert np.array_equal(ctxs[0].predict(b), ctxs[1].predict(b)), (it, b)
+    for c in ctxs:
+        c.close()
 
 
 def test_hmc_step_joint_refuses_std_normal_and_reports_shapes(Ctx):

@@ -65,6 +65,11 @@ def rel(a, b):
     ("ridge_base", dict(step_mode="random")),
     # Net::train_single_branch (net.rs:360-507)
     ("ridge_ard", dict(single_branch=True)),
+    # MCMCCfg::gradient_descent (line search over rss probes, branch_sampler.rs:964-1016)
+    ("ridge_ard", dict(gradient_descent=True, factor=1e-4)), ("lasso_ard", dict(gradient_descent=True, factor=1e-4)),
+    # MCMCCfg::gradient_descent_joint (params and precisions, 1019-1066)
+    ("ridge_ard", dict(gradient_descent_joint=True, factor=1e-5)),
+    ("lasso_base", dict(gradient_descent_joint=True, factor=1e-5)),
 ])
 def test_train_matches_oracle(prior, opts):
     from bann import MCMCConfig, Net
@@ -76,13 +81,15 @@ def test_train_matches_oracle(prior, opts):
     sampled_bias = opts.get("sampled_output_bias", False)
     factor = opts.get("factor", 1.0)
     single = opts.get("single_branch", False)
+    gd, gdj = opts.get("gradient_descent", False), opts.get("gradient_descent_joint", False)
     cfg = MCMCConfig(hmc_integration_length=10, chain_length=3, sampled_output_bias=sampled_bias,
                      hmc_step_size_factor=factor, hmc_step_size_mode=opts.get("step_mode", "izmailov"),
-                     joint_hmc=opts.get("joint_hmc", False))
+                     joint_hmc=opts.get("joint_hmc", False), gradient_descent=gd, gradient_descent_joint=gdj)
     (net.train_single_branch if single else net.train)(y, cfg)
     ora = NO.NetOracle(branches, X, hp)
     ora.train(y.astype(np.float64), d_ora, 3, 10, factor=factor, step_mode=opts.get("step_mode", "izmailov"),
-              sampled_output_bias=sampled_bias, joint_hmc=opts.get("joint_hmc", False), single_branch=single)
+              sampled_output_bias=sampled_bias, joint_hmc=opts.get("joint_hmc", False), single_branch=single,
+              gradient_descent=gd, gradient_descent_joint=gdj)
     assert d_dev.uniform() == d_ora.uniform(), "draw streams diverged (different number of draws)"
     s = net.summary()
     assert (s["num_samples"], s["num_accepted"], s["num_early_rejected"]) == (ora.ns, ora.nacc, ora.nearly)
@@ -246,6 +253,39 @@ def test_trace_trajectories_and_test_mse(tmp_path):
         o.close()
 
 
+def test_joint_training_writes_joint_trajectories(tmp_path):
+    """MCMCCfg::joint_hmc with MCMCCfg::trajectories: every hmc_step_joint writes
+    the joint Trajectory line (branch_sampler.rs:1126-1135, early rejections
+    included): per step the parameters, the precisions and the joint ldg
+    [params | precisions], the joint -H trace; the chain itself stays the
+    oracle's (recording does not change the launches' results)."""
+    from bann import MCMCConfig, Net
+    ctx, branches, X, y = build("ridge_ard")
+    hp = O.Hyper()
+    net = Net(ctx, (hp.dense, hp.summary, hp.output))
+    d_dev, d_ora = NO.Draws(11), NO.Draws(11)
+    net.set_rng(d_dev.uniform, d_dev.normal, d_dev.gamma)
+    L, chain = 6, 2
+    net.train(y, MCMCConfig(hmc_integration_length=L, chain_length=chain, hmc_step_size_factor=0.5, joint_hmc=True,
+                            trajectories=True), outdir=str(tmp_path))
+    trajs = [json.loads(t) for t in open(tmp_path / "traj").read().splitlines()]
+    assert len(trajs) == chain * 3
+    for t in trajs:
+        k = len(t["params"])
+        assert 1 <= k <= L and len(t["precisions"]) == k and len(t["ldg"]) == k and len(t["hamiltonian"]) == k + 1
+        P = len(t["params"][0])
+        Q = len(t["precisions"][0])
+        assert P in [ctx.num_params(b) for b in range(3)] and Q > 0 and len(t["ldg"][0]) == P + Q
+    ora = NO.NetOracle(branches, X, hp)
+    ora.train(y.astype(np.float64), d_ora, chain, L, factor=0.5, joint_hmc=True)
+    s = net.summary()
+    assert (s["num_samples"], s["num_accepted"], s["num_early_rejected"]) == (ora.ns, ora.nacc, ora.nearly)
+    for b, br in enumerate(ora.br):
+        assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < CHAIN_TOL, b
+    net.close()
+    ctx.close()
+
+
 def test_trajectory_recording_matches_oracle_hmc():
     """bann_set_trajectory_recording: the recorded parameters, gradients and -H of
     an injected-draw trajectory are the oracle's (params after each position
@@ -335,5 +375,59 @@ def test_perturb_predict_and_test_data_checks():
     with pytest.raises(BannError):   # n_test must be the test cohort's size (it sizes the prediction buffer)
         net.set_test_data(tctx, np.zeros(100, np.float32))
     net.set_test_data(tctx, np.zeros(250, np.float32))
+    for o in (net, ctx, tctx):
+        o.close()
+
+
+def test_net_gradient_r2s_rss_activations():
+    """the other callers of the boundary (SURVEY 8(b)): Net::gradient
+    (net.rs:520-527: every branch's log_density_gradient against the phenotype,
+    one packed launch), Net::branch_r2s (648-656, r2 = 1 - rss / sum y^2,
+    branch_sampler.rs:911-913), Net::rss / mse (637-646) and Net::activations
+    (509-518: forward_feed's activations of every layer) -- on the training
+    context and on another cohort -- against the oracle."""
+    from bann import BannContext, MCMCConfig, Net
+    ctx, branches, X, y = build("ridge_ard", seed=12)
+    net = Net(ctx, seed=4)
+    net.train(y, MCMCConfig(hmc_integration_length=5, chain_length=2, hmc_step_size_factor=0.5))
+    ms = (40, 64, 30)
+    rng = np.random.default_rng(5)
+    gt = O.synthetic_genotypes(rng, 500, sum(ms))
+    tctx = BannContext(0)
+    tctx.upload_genotypes(gt)
+    off = 0
+    for m, br in zip(ms, branches):
+        tctx.add_branch(np.arange(off, off + m, dtype=np.int32), br.layer_widths, "tanh", "ridge_ard")
+        off += m
+    tctx.finalize()
+    y_t = rng.normal(size=500).astype(np.float32)
+    mu, sd = tctx.genotype_stats()
+    Xt, off = [], 0
+    for m in ms:
+        s = np.arange(off, off + m)
+        off += m
+        Xt.append(x_std(gt[s], mu[s], sd[s]))
+    oracle_brs = []
+    for b, br in enumerate(branches):   # the net's current cfgs
+        ob = br.copy()
+        ob.weights, ob.biases = O.load_param_vec(ctx.get_params(b).astype(np.float64), br.num_markers, br.layer_widths)
+        O.load_precision_vec(ob, ctx.get_precisions(b).astype(np.float64))
+        oracle_brs.append(ob)
+    for c, XX, yy in ((None, X, y), (tctx, Xt, y_t)):
+        grads = net.gradient(yy, c)
+        r2 = net.branch_r2s(yy, c)
+        yd = yy.astype(np.float64)
+        for b, ob in enumerate(oracle_brs):
+            gw, gb, orss = O.log_density_gradient(ob, XX[b], yd)
+            assert norm_rel(grads[b], O.param_vec(gw, gb)) < 1e-5, b
+            assert abs(r2[b] - (1.0 - orss / float(yd @ yd))) <= 1e-5 * max(1.0, abs(r2[b])), b
+            acts = net.activations(b, c)
+            _, oacts = O.forward_feed(ob, XX[b])
+            assert len(acts) == len(oacts)
+            for a, oa in zip(acts, oacts):
+                assert a.shape == oa.shape and norm_rel(a, oa) < 1e-5, b
+        f = sum(O.predict(ob, xx) for ob, xx in zip(oracle_brs, XX)) + net.summary()["output_bias"]
+        orss = float(np.sum((yd - f) ** 2))
+        assert rel(net.rss(yy, c), orss) < 1e-5 and rel(net.mse(yy, c), orss / yy.size) < 1e-5
     for o in (net, ctx, tctx):
         o.close()
