@@ -42,6 +42,7 @@ void refresh_state(bann_ctx* ctx) {
   DevState& s = ctx->st;
   s.br = ctx->d_br;
   s.xu2 = ctx->d_xu2;
+  s.xi = ctx->d_xi;
   s.dig = ctx->d_dig;
   s.fc = ctx->d_fc;
   s.mu = ctx->d_mub;
@@ -228,12 +229,19 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     }
     const int spi = 1;  // partial slabs per work item
     const int ns = solo ? h.solo_items : d.nsplits;
+    if (grp->items.empty()) grp->fi = true;
+    if (d.fused == 1) {
+      grp->fi = grp->fi && d.xi_off >= 0;
+      grp->max_seg = std::max(grp->max_seg, (d.nchunks + 3) / 4);
+    }
     for (int s = 0; s < ns; ++s) {  // splits on tile (4-fragment) boundaries
-      GradItem it;
+      GradItem it{};
       it.branch = b;
       it.split = s;
       it.frag_begin = (int32_t)(BANN_TILE_FRAGS * (ntile * s / ns));
       it.frag_end = (int32_t)std::min<int64_t>(nfrag, BANN_TILE_FRAGS * (ntile * (s + 1) / ns));
+      it.tile0 = (int32_t)grp->tiles;
+      grp->tiles += ((it.frag_end + 3) >> 2) - (it.frag_begin >> 2);
       it.part_at = solo ? solo_part + (int64_t)s * spi * h.P : d.part_off + (int64_t)s * spi * h.P;
       it.rss_at = solo ? solo_rss + (int64_t)s * spi : (int64_t)b * ctx->max_splits + (int64_t)s * spi;
       grp->items.push_back(it);
@@ -379,6 +387,8 @@ int run_forward(bann_ctx* ctx, const Plan& p) {
       launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, 1, ctx->stream);
     else if (g.kind == 3)
       launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, 1, ctx->stream);
+    else if (g.fi)
+      launch_forward_fi(s, g.d_items, ni, g.tiles, g.L, g.act, g.max_seg, ctx->cus, ctx->stream);
     else
       launch_forward_fx(s, g.d_items, ni, g.L, g.act, g.full, ctx->stream);
   }
@@ -456,7 +466,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
     (void)hipFree(ctx->d_dbg);
   }
   free_plan(ctx->lf);
-  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xu2, ctx->d_dig, ctx->d_fc, ctx->d_mub,
+  void* bufs[] = {ctx->d_g, ctx->d_mu, ctx->d_sigma, ctx->d_br, ctx->d_xu2, ctx->d_xi, ctx->d_dig, ctx->d_fc, ctx->d_mub,
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
@@ -738,6 +748,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
     cus = 256;
+  ctx->cus = cus;
   // Splits: whole rounds of resident workgroups.  All items of a packed launch
   // are equally long, so a launch costs ceil(items / slots) rounds of (per-item
   // prologue/epilogue + tiles per wave); choose the split count minimising that
@@ -777,6 +788,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     fxl_splits[nw] = best_splits(nfxl[nw], per_cu * cus, 1);
   }
   int64_t q_off = 0;
+  // forward-only fi images (kernels_fi.hip) for the fx branches; BANN_FWD_FI=0: the LDS forward
+  const bool fi_on = !(getenv("BANN_FWD_FI") && atoi(getenv("BANN_FWD_FI")) == 0);
+  int64_t xi_off = 0;
   int64_t x2_off = 0, dig_off = 0, p_off = 0, mk_off = 0, part_off = 0, scr_off = 0, items = 0;
   // gx scratch groups: branches in index order until the budget (BANN_GX_SCRATCH_MB,
   // default a quarter of the free device memory, at most 64 GiB) is full; every
@@ -798,6 +812,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     BranchDev& d = h.dev;
     d.x_off = x2_off;  // byte offset of the branch's 2-bit tile image: [tile][chunk][1 KiB]
     x2_off += ntile * d.nchunks * 1024;
+    d.xi_off = -1;  // fx branches: the individual-major image of the forward-only pass, [frag][segment][1 KiB]
+    if (d.fused == 1 && fi_on) {
+      d.xi_off = xi_off;
+      xi_off += 4 * ntile * ((d.nchunks + 3) / 4) * 1024;
+    }
     d.dig_off = dig_off;
     if (d.fused) dig_off += (int64_t)d.nchunks * 1024 * (d.fused == 2 ? 8 : 1);
     d.p_off = p_off;
@@ -900,6 +919,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   ctx->total_q = q_off;
   const int64_t nb = (int64_t)ctx->br.size();
   CK(dalloc(&ctx->d_xu2, x2_off));
+  ctx->xi_bytes = xi_off;
+  if (xi_off > 0) CK(dalloc(&ctx->d_xi, xi_off));
   CK(dalloc(&ctx->d_dig, dig_off));
   CK(hipMemsetAsync(ctx->d_dig, 0, (size_t)std::max<int64_t>(dig_off, 1), ctx->stream));
   CK(dalloc(&ctx->d_fc, nb));
@@ -978,6 +999,23 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipMemcpyAsync(d_idx, allidx.data(), allidx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(d_jobs, jobs.data(), jobs.size() * sizeof(PackJob), hipMemcpyHostToDevice, ctx->stream));
   launch_pack_tiles(ctx->d_g, ctx->rowb, d_jobs, (int32_t)jobs.size(), d_idx, ntile, ctx->d_xu2, ctx->stream);
+  PackJob* d_fijobs = nullptr;
+  if (ctx->d_xi) {  // the fi images: one job per (branch, 256-marker segment)
+    std::vector<PackJob> fj;
+    int32_t base = 0;
+    for (auto& h : ctx->br) {
+      const int nseg = (h.dev.nchunks + 3) / 4;
+      if (h.dev.xi_off >= 0)
+        for (int sg = 0; sg < nseg; ++sg)
+          fj.push_back(PackJob{h.dev.xi_off + 1024ll * sg, 1024ll * nseg, base + 256 * sg,
+                               std::min(256, h.m - 256 * sg)});
+      base += h.m;
+    }
+    CK(dalloc(&d_fijobs, (int64_t)fj.size()));
+    CK(hipMemcpyAsync(d_fijobs, fj.data(), fj.size() * sizeof(PackJob), hipMemcpyHostToDevice, ctx->stream));
+    launch_pack_fi(ctx->d_g, ctx->rowb, d_fijobs, (int32_t)fj.size(), d_idx, ntile, ctx->d_xi, ctx->stream);
+    CK(hipStreamSynchronize(ctx->stream));  // fj goes out of scope
+  }
   launch_gather_stats(ctx->d_mu, ctx->d_sigma, d_idx, (int32_t)allidx.size(), ctx->d_mub, ctx->d_sigb, ctx->stream);
   CK(hipGetLastError());
   std::vector<BranchDev> descs;
@@ -1000,6 +1038,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipStreamSynchronize(ctx->stream));  // host vectors go out of scope
   dfree(d_idx);
   dfree(d_jobs);
+  dfree(d_fijobs);
   CK(dalloc(&ctx->d_br, nb));
   CK(hipMemcpyAsync(ctx->d_br, descs.data(), nb * sizeof(BranchDev), hipMemcpyHostToDevice, ctx->stream));
   CK(hipMemcpyAsync(ctx->d_eprec, eprec.data(), nb * sizeof(float), hipMemcpyHostToDevice, ctx->stream));

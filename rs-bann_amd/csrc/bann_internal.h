@@ -27,6 +27,7 @@ struct BranchDev {
   int64_t dig_off;    // byte offset of the MFMA A-operand digits [nchunks][64][16]
   int64_t y_off;      // offset of the target / prediction vectors (b * n)
   int64_t scr_off;    // gx path: float offset of the branch's scratch within its scratch group
+  int64_t xi_off;     // byte offset of the individual-major fi image (kernels_fi.hip), -1 if none
   int32_t m;          // markers in the branch
   int32_t nchunks;    // ceil(m / 64)
   int32_t L;          // number of layers (weight matrices)
@@ -72,6 +73,8 @@ struct GradItem {
   int32_t frag_end;
   int64_t part_at;  // float offset in DevState::part of the item's (first) slab
   int64_t rss_at;   // index in DevState::rss_part of its (first) rss partial
+  int32_t tile0;    // forward-only fi pass: the group's tiles before this item (its index space)
+  int32_t pad_;
 };
 // solo-mode fold: a branch's ns slabs at part[part] / rss_part[rss] -> its slab 0
 struct FoldJob {
@@ -90,6 +93,7 @@ struct FusedConst {
 struct DevState {
   const BranchDev* br;    // [nbranch]
   const uint8_t* xu2;     // 2-bit genotype tile images of every branch ([tile][chunk][1 KiB], kernels_fx.hip)
+  const uint8_t* xi;      // individual-major 2-bit images of the fx branches (kernels_fi.hip), or null
   const uint8_t* dig;     // digits
   FusedConst* fc;         // [nbranch]
   const float* mu;        // gathered per-branch marker means  [sum m]
@@ -195,6 +199,11 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 // forward-only fx pass (predictions into st.pred, no target / backward / partials)
 void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act, int full8,
                        hipStream_t s);
+// forward-only fx pass over the individual-major fi images (kernels_fi.hip)
+void launch_forward_fi(const DevState& st, const GradItem* items, int32_t nitems, int64_t total_tiles, int32_t L,
+                       int32_t act, int32_t max_seg, int32_t cus, hipStream_t s);
+void launch_pack_fi(const uint8_t* raw, int64_t rowb, const PackJob* jobs, int32_t njobs, const int32_t* idx,
+                    int64_t ntile, uint8_t* dst, hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                            int32_t nw, int full, int write_pred, hipStream_t s);
 int fxl_lds_bytes(int nw, int nl);

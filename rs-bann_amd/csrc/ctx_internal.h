@@ -27,6 +27,9 @@ struct BranchHost {
 struct LaunchGroup {
   int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
   int32_t L = 0, act = 0, nw = 1, full = 0;
+  int64_t tiles = 0;    // fx: the items' 64-individual tiles (the fi forward's index space, GradItem::tile0)
+  int32_t max_seg = 1;  // fx: the largest 256-marker segment count of its branches
+  bool fi = false;      // fx: every branch has an individual-major fi image (kernels_fi.hip)
   std::vector<GradItem> items;
   GradItem* d_items = nullptr;
 };
@@ -76,6 +79,9 @@ struct bann_ctx {
   // device buffers
   BranchDev* d_br = nullptr;
   uint8_t* d_xu2 = nullptr;  // 2-bit genotype tile images of every branch (u2t, kernels_fx.hip)
+  uint8_t* d_xi = nullptr;   // individual-major 2-bit images of the fx branches (kernels_fi.hip; BANN_FWD_FI=0: none)
+  int64_t xi_bytes = 0;
+  int32_t cus = 256;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;

@@ -47,7 +47,11 @@ __device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(u
 // the data lands at M0 + 16 * lane (4 * lane for the dword form).
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
+#if BANN_GLDS_NT  // non-temporal genotype stream (profiling switch)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m0), "v"(gsrc) : "memory", "m0");
+#else
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");
+#endif
 }
 __device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));

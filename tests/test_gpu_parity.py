@@ -1010,3 +1010,37 @@ def test_upload_paths_agree_and_reject_non_2bit(Ctx):
     with pytest.raises(BannError):
         c.upload_genotypes(bad)
     c.close()
+
+
+@pytest.mark.parametrize("n", [1000, 4093])
+def test_forward_fi_matches_lds_forward(Ctx, n, monkeypatch):
+    """the forward-only pass over the individual-major fi images
+    (kernels_fi.hip: plain global loads into the i8 MFMA, the group's tiles cut
+    into equal per-wave ranges across branch boundaries) gives the bits of the
+    LDS forward (k_forward_fx, BANN_FWD_FI=0) for every fx shape -- one and two
+    256-marker segments, 2 to 4 layers, every activation -- and the oracle's
+    predictions (forward_feed, branch_sampler.rs:743-782)."""
+    rng = np.random.default_rng(n)
+    shapes = [(60, [4, 4, 1], "tanh"), (256, [4, 1], "relu"), (300, [3, 4, 1], "silu"), (512, [4, 4, 4, 1], "tanh"),
+              (17, [2, 3, 1], "leaky_relu"), (500, [4, 4, 1], "identity"), (129, [4, 4, 1], "tanh")]
+    g = O.synthetic_genotypes(rng, n, sum(m for m, _, _ in shapes))
+    specs, off = [], 0
+    for m, w, act in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, act=act)), y=np.zeros(n)))
+        off += m
+    preds = []
+    for fi in ("0", "1"):
+        monkeypatch.setenv("BANN_FWD_FI", fi)
+        ctx = build_context(Ctx, g, specs)
+        assert all(ctx.kernel_path(b) == "fused" for b in range(len(specs)))
+        preds.append(ctx.predict_many(list(range(len(specs)))))
+        if fi == "1":
+            sub = ctx.predict_many([5, 1, 3])   # another plan: other items, other cut points
+            assert np.array_equal(sub, preds[1][[5, 1, 3]])
+            mu, sd = ctx.genotype_stats()
+            for b, s in enumerate(specs):
+                X = x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]])
+                assert norm_rel(preds[1][b], O.predict(s["branch"], X)) < 1e-5, b
+        ctx.close()
+    assert np.array_equal(preds[0], preds[1])

@@ -99,10 +99,18 @@ def test_train_matches_oracle(prior, opts):
         assert rel(a, b) < CHAIN_TOL, (mse, ora.mse)
     for a, b in zip(lpd, ora.lpd):
         assert rel(a, b) < CHAIN_TOL, (lpd, ora.lpd)
+    # gradient descent: where the ascent direction raises the rss, the halving line
+    # search (branch_sampler.rs:983-989) runs until a halved step stops lowering the
+    # rss -- in f32 (device and reference) where the probe's change sinks below the
+    # rounding of the rss (steps ~1e-9), in the float64 oracle at ~1e-17 (measured
+    # step by step: tools/diag/gd_trace.py).  Both stopping steps move theta by
+    # < 1e-8 relative, but the chain feeds the difference back through the Gibbs
+    # draws: 6e-4 after 3 sweeps of lasso_ard, hence 1e-3 for the parameters there.
+    ptol = 1e-3 if (gd or gdj) else CHAIN_TOL
     for b, br in enumerate(ora.br):
-        assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < CHAIN_TOL, b
-        assert norm_rel(ctx.get_precisions(b), O.precision_vec(br)) < CHAIN_TOL, b
-    assert norm_rel(net.residual(), ora.residual) < CHAIN_TOL
+        assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < ptol, b
+        assert norm_rel(ctx.get_precisions(b), O.precision_vec(br)) < ptol, b
+    assert norm_rel(net.residual(), ora.residual) < ptol
     assert abs(s["output_bias"] - ora.ob_bias) <= CHAIN_TOL * max(1.0, abs(ora.ob_bias))
     assert rel(s["error_precision"], ora.g_eprec) < CHAIN_TOL
     assert rel(s["output_reg_sum"], ora.g_reg) < CHAIN_TOL
