@@ -252,6 +252,19 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       solo_rss += (int64_t)ns * spi;
     }
   }
+  {  // the fused update (kernels_fx.hip tail): fx branches only, the small update, one round of items
+    int64_t items = 0;
+    bool ok = !solo && p.gx.empty() && ctx->d_upd_cnt != nullptr && ctx->fuse_update_on;
+    for (const auto& g : p.groups) {
+      ok = ok && g.kind == 1;
+      items += (int64_t)g.items.size();
+    }
+    for (int i = 0; i < nb && ok; ++i) {
+      const BranchHost& h = ctx->br[branches[i]];
+      ok = h.P <= 2048 && h.m <= 512 && !update_is_large(h.dev);
+    }
+    p.fuse_update = ok && items > 0 && items <= 2ll * ctx->cus;
+  }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
   std::stable_sort(p.gx.begin(), p.gx.end(),
                    [&](int32_t a, int32_t b) { return ctx->br[a].gx_group < ctx->br[b].gx_group; });
@@ -346,10 +359,13 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
 // write_pred: 0 = no predictions (the layered path writes them anyway), 1 = the
 // predictions f_b(theta) into pred, 2 = into pred0 (a trajectory's start: the
 // restore copy and the residual change read them there)
-int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
+// upd_mode >= 0 (a plan with fuse_update): the leapfrog update of that mode and
+// step runs in the fx launch's tail -- the caller launches no update (run_grad_update)
+int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode, int upd_step) {
   DevState s = ctx->st;
   if (write_pred == 2) s.pred = ctx->d_pred0;
   const int wp = write_pred != 0;
+  int32_t* cnt = upd_mode >= 0 ? ctx->d_upd_cnt : nullptr;
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
@@ -357,7 +373,7 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred) {
     else if (g.kind == 3)
       launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, wp, ctx->stream);
     else
-      launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, ctx->stream);
+      launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, upd_mode, upd_step, cnt, ctx->stream);
   }
   if (!p.fold.empty()) launch_fold_solo(s, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
   // gx branches: scratch group by scratch group (the groups reuse one scratch)
@@ -445,6 +461,7 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   bann_ctx* ctx = new bann_ctx();
   ctx->device = device;
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
+  if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_on = atoi(e) != 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return BANN_E_HIP;
@@ -472,7 +489,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
                   ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_fold_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
-                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res,
+                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt,
                   ctx->d_res_part};
   for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
   clear_graphs(ctx);
@@ -967,6 +984,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipMemsetAsync(ctx->d_pred0, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_scr, scr_off));
   CK(dalloc(&ctx->d_eprec, nb));
+  CK(dalloc(&ctx->d_upd_cnt, nb));
+  CK(hipMemsetAsync(ctx->d_upd_cnt, 0, nb * sizeof(int32_t), ctx->stream));
   CK(dalloc(&ctx->d_u, nb));
   CK(dalloc(&ctx->d_h0, nb));
   CK(dalloc(&ctx->d_ld, nb));
@@ -1828,6 +1847,23 @@ extern "C" int bann_network_timing(bann_ctx* ctx, float* forward_ms, float* allr
 
 extern "C" int64_t bann_ctx_num_individuals(const bann_ctx* ctx) { return ctx ? ctx->n : BANN_E_ARG; }
 
+// one leapfrog step of a session: the gradient launch and the update (fused into
+// the gradient launch's tail for a fuse_update plan; launch timing then books
+// both on the gradient)
+static int grad_update(bann_ctx* ctx, const Plan& p, int write_pred, int mode, int step) {
+  if (p.fuse_update) {
+    mark_predictions(ctx, p, false);  // theta moves
+    int rc = run_grad(ctx, p, write_pred, mode, step);
+    tm_mark(ctx, TM_GRAD1);
+    return rc;
+  }
+  int rc = run_grad(ctx, p, write_pred);
+  if (rc) return rc;
+  tm_mark(ctx, TM_GRAD1);
+  run_update(ctx, p, mode, step);
+  return BANN_OK;
+}
+
 extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32_t nb, int32_t L, float max_dh,
                                    int32_t step_mode, float factor, uint64_t seed) {
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
@@ -1843,10 +1879,8 @@ extern "C" int bann_leapfrog_begin(bann_ctx* ctx, const int32_t* branches, int32
   rc = traj_prepare(ctx, ctx->lf, L, max_dh, step_mode, factor, nullptr, nullptr, seed, nullptr);
   if (rc) return rc;
   tm_mark(ctx, TM_GRAD0);
-  rc = run_grad(ctx, ctx->lf, 2);  // f(theta_0) straight into pred0 (the restore copy and the residual change)
+  rc = grad_update(ctx, ctx->lf, 2, MODE_INIT, 0);  // f(theta_0) straight into pred0 (the restore copy and the residual change)
   if (rc) return rc;
-  tm_mark(ctx, TM_GRAD1);
-  run_update(ctx, ctx->lf, MODE_INIT, 0);
   tm_mark(ctx, TM_UPD1);
   CK(hipGetLastError());
   ctx->lf_active = true;
@@ -1861,10 +1895,8 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
     tm_mark(ctx, TM_GRAD0);
-    int rc = run_grad(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0);
+    int rc = grad_update(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
     if (rc) return rc;
-    tm_mark(ctx, TM_GRAD1);
-    run_update(ctx, ctx->lf, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
     tm_mark(ctx, TM_UPD1);
   }
   CK(hipGetLastError());

@@ -194,8 +194,10 @@ void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, ui
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int mode,
                           int nch, int write_pred, hipStream_t s);
 bool wx_exact();
+// upd_cnt != null: the fused leapfrog update (mode, step) in the tail -- the last workgroup of
+// each branch updates it (update_core.h); upd_cnt = one zeroed arrival counter per branch
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int full8, int write_pred, hipStream_t s);
+                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt, hipStream_t s);
 // forward-only fx pass (predictions into st.pred, no target / backward / partials)
 void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act, int full8,
                        hipStream_t s);

@@ -57,6 +57,10 @@ struct Plan {
   int32_t* d_gx = nullptr;
   int32_t* d_gxpre = nullptr;
   bool owns = false;
+  // every branch fx-shaped with the small update (P <= 2048, m <= 512), one round of
+  // work items, no solo re-split: the leapfrog session runs the update in the
+  // gradient launch's tail (kernels_fx.hip, BANN_FUSE_UPDATE=0: separate launches)
+  bool fuse_update = false;
 };
 
 struct bann_ctx {
@@ -82,6 +86,8 @@ struct bann_ctx {
   uint8_t* d_xi = nullptr;   // individual-major 2-bit images of the fx branches (kernels_fi.hip; BANN_FWD_FI=0: none)
   int64_t xi_bytes = 0;
   int32_t cus = 256;
+  int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
+  bool fuse_update_on = true;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;
@@ -193,7 +199,7 @@ void refresh_state(bann_ctx* ctx);
 bool check_branch(const bann_ctx* ctx, int32_t b);
 int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool persistent);
 void free_plan(Plan& p);
-int run_grad(bann_ctx* ctx, const Plan& p, int write_pred);
+int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode = -1, int upd_step = 0);
 int run_forward(bann_ctx* ctx, const Plan& p);  // predictions only
 void run_update(bann_ctx* ctx, const Plan& p, int32_t mode, int32_t step);
 int ensure_htrace(bann_ctx* ctx, int32_t L);

@@ -47,7 +47,10 @@ __device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(u
 // the data lands at M0 + 16 * lane (4 * lane for the dword form).
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
-#if BANN_GLDS_NT  // non-temporal genotype stream (profiling switch)
+#ifndef BANN_GLDS_NT
+#define BANN_GLDS_NT 1  // the genotype / target streams are read once per launch: non-temporal (-2 % fx, A/B)
+#endif
+#if BANN_GLDS_NT
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m0), "v"(gsrc) : "memory", "m0");
 #else
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(gsrc) : "memory", "m0");

@@ -43,6 +43,7 @@
 #include "activations.h"
 #include "bann_internal.h"
 #include "kernel_util.h"
+#include "update_core.h"
 
 #define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
 #define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
@@ -127,7 +128,8 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 
 template <int NL, int ACT, int NCH>
 __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
-    k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred) {
+    k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred, int upd_mode, int upd_step,
+                    int32_t* __restrict__ upd_cnt) {
   constexpr int NH = NL - 1;  // layers with activations
   constexpr int NW = FX_WAVES;
   constexpr int NS = 8 + (NH - 1) * 20;  // head statistics per wave
@@ -535,31 +537,53 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   }
   if (wave == 0 && lane == 0)
     st.rss_part[it.rss_at] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
-}
-
-template <int NL, int NCH>
-static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, hipStream_t s) {
-  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
-  switch (act) {
-    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp); break;
-    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp); break;
-    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp); break;
-    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp); break;
-    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp); break;
+  if (upd_cnt) {
+    // fused leapfrog update (a one-round launch, bann_api.hip build_plan): the
+    // last of the branch's split workgroups to finish updates it here, with the
+    // update kernel's arithmetic and reduction order (update_small as 512 virtual
+    // threads), instead of a second launch.  Release the partials, count the
+    // arrival, acquire the other workgroups' partials.
+    __shared__ int s_last;
+    __shared__ double s_redd[4 * 8];
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&upd_cnt[b], 1) == bd.nsplits - 1;
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      if (threadIdx.x == 0) upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
+      float* s_th = reinterpret_cast<float*>(&s_x[0][0][0]);  // the tile slots are free: P <= 2048 floats
+      update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
+    }
   }
 }
 
-// full8: every branch of this launch group has exactly 8 chunks
+template <int NL, int NCH>
+static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, int um, int us,
+                         int32_t* cnt, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
+  switch (act) {
+    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+  }
+}
+
+// full8: every branch of this launch group has exactly 8 chunks; upd_cnt != null:
+// the fused leapfrog update in the launch's tail (mode upd_mode, step upd_step)
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int full8, int write_pred, hipStream_t s) {
+                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt, hipStream_t s) {
   if (nitems <= 0) return;
+  const int wp = write_pred, um = upd_mode, us = upd_step;
   switch (L * 2 + (full8 ? 1 : 0)) {
-    case 4: launch_fx_nl<2, 0>(st, items, nitems, act, write_pred, s); break;
-    case 5: launch_fx_nl<2, 8>(st, items, nitems, act, write_pred, s); break;
-    case 6: launch_fx_nl<3, 0>(st, items, nitems, act, write_pred, s); break;
-    case 7: launch_fx_nl<3, 8>(st, items, nitems, act, write_pred, s); break;
-    case 8: launch_fx_nl<4, 0>(st, items, nitems, act, write_pred, s); break;
-    case 9: launch_fx_nl<4, 8>(st, items, nitems, act, write_pred, s); break;
+    case 4: launch_fx_nl<2, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 5: launch_fx_nl<2, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 6: launch_fx_nl<3, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 7: launch_fx_nl<3, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 8: launch_fx_nl<4, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 9: launch_fx_nl<4, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
     default: break;
   }
 }

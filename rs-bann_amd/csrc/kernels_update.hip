@@ -121,324 +121,7 @@ __device__ void refresh_fused_const(const DevState& st, int b, const BranchDev& 
   }
 }
 
-// NV doubles summed over the workgroup in one pass (one barrier pair)
-template <int NT, int NV>
-__device__ void block_sum_n(double (&v)[NV], double* red) {
-#pragma unroll
-  for (int q = 0; q < NV; ++q)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int q = 0; q < NV; ++q) red[q * (NT / 64) + w] = v[q];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NV; ++q) {
-    double t = 0.0;
-    for (int k = 0; k < NT / 64; ++k) t += red[q * (NT / 64) + k];
-    v[q] = t;
-  }
-}
-
-// Register-resident update of a fused branch (P <= UPD_CAP * NT, m <= MPT * NT, <= 4
-// first-layer columns, or a wide branch with <= 32: every C2/C3/C4/C5 branch).  All global loads of the
-// step are issued up front (partials, theta, lambda, momentum, eps, theta0,
-// mu, sigma), the parameters stay in registers between the reduction and the
-// position step, and the W0-digit refresh reads the new W0 from LDS: two
-// memory latencies and two workgroup reductions per launch instead of about
-// seven dependent global round trips (the launch follows a genotype stream that
-// has evicted all of it from L2).  Same arithmetic as the general path below.
-#define UPD_CAP 8
-// parameters per thread: the 512-thread kernel only takes P <= 2048 (update_is_large
-// sends the rest to the 1024-thread one), so 4 -- 20 fewer VGPRs, same bits
-template <int NT>
-constexpr int upd_cap() { return NT == 512 ? 4 : UPD_CAP; }
-template <int NT, int MPT>
-__device__ void update_small(const DevState& st, int b, const BranchDev& bd, int mode, bool prof, int step,
-                             double* redd, float* s_th) {
-  const int P = bd.P, m = bd.m, w0 = bd.widths[0];
-  const int64_t base = bd.p_off;
-  const int t = threadIdx.x;
-  // a finished trajectory (STEP / LAST after an early rejection) is left alone; the
-  // status is checked after every load of the step has been issued, not before
-  const bool check = !prof && (mode == MODE_STEP || mode == MODE_LAST);
-  const int status = st.status[b];
-  // marker statistics for the refresh, prefetched
-  float mus[MPT], sgs[MPT];
-#pragma unroll
-  for (int c = 0; c < MPT; ++c) {
-    const int j = t + c * NT;
-    mus[c] = j < m ? st.mu[bd.mk_off + j] : 0.f;
-    sgs[c] = j < m ? st.sigma[bd.mk_off + j] : 0.f;
-  }
-  double rss = 0.0;
-  for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
-  const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
-  const bool lasso = (bd.prior == 2 || bd.prior == 3);
-  constexpr int CAP = upd_cap<NT>();
-  float th[CAP], gr[CAP], pm[CAP], ep[CAP], t0[CAP];
-  double sums[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int c = 0; c < CAP; ++c) {
-    const int i = t + c * NT;
-    th[c] = gr[c] = pm[c] = ep[c] = t0[c] = 0.f;
-    if (i >= P) continue;
-    float d = 0.f;
-    for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
-    th[c] = st.theta[base + i];
-    const float lm = st.lam[base + i];
-    const float ll = st.lamld[base + i];
-    pm[c] = st.mom[base + i];
-    ep[c] = st.eps[base + i];
-    if (mode == MODE_STEP || mode == MODE_LAST) t0[c] = st.theta0[base + i];
-    const float sgn = th[c] > 0.f ? 1.f : (th[c] < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
-    const float reg = lasso ? lm * sgn : lm * th[c];
-    gr[c] = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
-    sums[0] -= lasso ? (double)ll * fabs((double)th[c]) : 0.5 * (double)ll * (double)th[c] * (double)th[c];
-    if (mode == MODE_INIT) {
-      sums[1] += (double)pm[c] * (double)pm[c];
-    } else if (mode != MODE_GRAD) {  // second half step of this leapfrog step (momentum.rs:121-136)
-      pm[c] = pm[c] + ep[c] * 0.5f * gr[c];
-      sums[1] += (double)pm[c] * (double)pm[c];
-      sums[2] += ((double)th[c] - (double)t0[c]) * (double)pm[c];
-    }
-  }
-  if (check && status != ST_RUNNING) return;
-  if (!prof)
-#pragma unroll
-    for (int c = 0; c < CAP; ++c)
-      if (t + c * NT < P) st.grad[base + t + c * NT] = gr[c];
-  if (mode == MODE_GRAD) {
-    double v1[1] = {sums[0]};
-    block_sum_n<NT, 1>(v1, redd);
-    if (t == 0) {
-      st.ld_out[b] = v1[0] - (double)le * rss / 2.0;
-      st.rss_out[b] = rss;
-    }
-    return;
-  }
-  block_sum_n<NT, 3>(sums, redd);
-  // + log_density_wrt_rss (100-102); network mode: the rss term is added once for the network by the host
-  const double ld = sums[0] - (st.netmode ? 0.0 : (double)le * rss / 2.0);
-  const double h = ld - 0.5 * sums[1];                   // -H (878-883)
-  const int stride = st.lint + 1;
-  // what happens to theta: 0 = position step, 1 = restore theta0, 2 = keep
-  int act = 0;
-  if (mode == MODE_INIT) {
-    if (t == 0) {
-      st.h0[b] = h;
-      st.htrace[(int64_t)b * stride] = h;
-      st.status[b] = ST_RUNNING;
-      st.uturn[b] = -1;
-      st.rss_out[b] = rss;
-      st.ld_out[b] = ld;
-    }
-  } else {
-    const double h0 = st.h0[b];
-    const bool diverged = !prof && !st.netmode && fabs(h - h0) > (double)st.max_dh;
-    if (!prof && t == 0) st.htrace[(int64_t)b * stride + step] = h;
-    if (diverged) {  // RejectedEarly (1264-1279)
-      act = 1;
-      if (t == 0) st.status[b] = ST_REJECTED_EARLY;
-    } else {
-      if (!prof && t == 0 && sums[2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;  // 1281-1284
-      if (mode == MODE_LAST && st.netmode) {  // network mode: the host decides for the network
-        act = 2;
-        if (t == 0) {
-          st.ld_out[b] = ld;
-          st.rss_out[b] = rss;
-        }
-      } else if (mode == MODE_LAST) {  // Metropolis (928-962)
-        const double log_acc = h - h0;
-        const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
-        const bool accept = (double)st.uacc[b] < acc_p;
-        act = accept ? 2 : 1;
-        if (t == 0) {
-          st.status[b] = accept ? ST_ACCEPTED : ST_REJECTED;
-          st.ld_out[b] = ld;
-          st.rss_out[b] = rss;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < CAP; ++c) {
-    const int i = t + c * NT;
-    if (i >= P) continue;
-    float tn = th[c];
-    if (act == 0) {  // (next) first half step + position step (params.rs:728-738)
-      const float p = pm[c] + 0.5f * ep[c] * gr[c];
-      tn = th[c] + ep[c] * p;
-      if (prof) {
-        st.grad[base + i] = tn;  // same traffic, chain unchanged
-        tn = th[c];
-      } else {
-        st.mom[base + i] = p;
-        st.theta[base + i] = tn;
-        if (mode == MODE_INIT) st.theta0[base + i] = th[c];
-      }
-    } else {
-      if (mode != MODE_INIT && !prof) st.mom[base + i] = pm[c];  // the half-stepped momentum
-      if (act == 1) {
-        tn = t0[c];
-        st.theta[base + i] = tn;
-      }
-    }
-    s_th[i] = tn;
-  }
-  __syncthreads();
-  // ---- W0 digit refresh from the new W0 in LDS (the general refresh_fused_const),
-  // four columns per pass (wide branches: eight passes, digit image of 8 column blocks) ----
-  const float* W0 = s_th + bd.woff[0];
-  const float* b0 = s_th + bd.boff[0];
-  const int NB = bd.fused == 2 ? 8 : 1;
-  uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
-  __shared__ float s_mx[4][NT / 64];
-  __shared__ double s_cs[4][NT / 64];
-  const int wv = t >> 6;
-  if (NT == 1024 && NB == 8 && m <= 128) {
-    // wide branches (C5: m = 125, w0 = 32): the eight four-column passes run side by
-    // side -- thread t takes marker t & 127 of column quad t >> 7 (waves 2q, 2q + 1),
-    // one barrier instead of sixteen.  The lane -> marker map and the reduction order
-    // are those of the pass loop below, so every bit of the digits, scales and c0 is too.
-    const int j = t & 127, kq = t >> 7;
-    const bool on = j < m;
-    const float sg = on ? st.sigma[bd.mk_off + j] : 0.f;
-    const float mu = on ? st.mu[bd.mk_off + j] : 0.f;
-    float mx[4], wq[4];
-    double cs[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = 4 * kq + q;
-      wq[q] = (on && k < w0 && sg > 0.f) ? W0[k * m + j] / sg : 0.f;
-      mx[q] = fmaxf(0.f, fabsf(wq[q]));
-      cs[q] = 0.0;
-      if (on && k < w0) cs[q] += (double)mu * (double)wq[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
-        cs[q] += __shfl_xor(cs[q], o);
-      }
-    __shared__ float s_mx8[NT / 64][4];
-    __shared__ double s_cs8[NT / 64][4];
-    if ((t & 63) == 0)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        s_mx8[wv][q] = mx[q];
-        s_cs8[wv][q] = cs[q];
-      }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = 4 * kq + q;
-      // (+ the other waves' zeros, as the pass loop adds them)
-      const float M = fmaxf(fmaxf(s_mx8[2 * kq][q], s_mx8[2 * kq + 1][q]), 0.f);
-      const double C = (s_cs8[2 * kq][q] + s_cs8[2 * kq + 1][q]) + 0.0;
-      float sc = 1.f;  // s = 2^e with max/s <= 127
-      if (M > 0.f) {
-        int e;
-        frexpf(M / 127.f, &e);
-        sc = ldexpf(1.f, e);
-      }
-      if (j == 0 && k < w0) {
-        st.fc[b].scale[k] = sc;
-        st.fc[b].c0[k] = (float)((double)b0[k] - C);
-      }
-      if (on && k < w0) {
-        double v = (double)wq[q] * (1.0 / (double)sc);
-        const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const double r = rint(v);
-          dig[((((int64_t)ch * NB + kq) * 64 + 16 * grp + 4 * q + d) * 16) + jj] = (uint8_t)(int8_t)r;
-          v = (v - r) * 128.0;
-        }
-      }
-    }
-    return;
-  }
-  for (int k0 = 0; k0 < w0; k0 += 4) {
-    const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
-    float mx[4] = {0.f, 0.f, 0.f, 0.f};
-    double cs[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int c = 0; c < MPT; ++c) {
-      const int j = t + c * NT;
-      if (j >= m) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (q < nk) {
-          const float wp = sgs[c] > 0.f ? W0[(k0 + q) * m + j] / sgs[c] : 0.f;
-          mx[q] = fmaxf(mx[q], fabsf(wp));
-          cs[q] += (double)mus[c] * (double)wp;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
-        cs[q] += __shfl_xor(cs[q], o);
-      }
-    if ((t & 63) == 0)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        s_mx[q][wv] = mx[q];
-        s_cs[q][wv] = cs[q];
-      }
-    __syncthreads();
-    double inv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float M = s_mx[q][0];
-      double C = s_cs[q][0];
-      for (int w = 1; w < NT / 64; ++w) {
-        M = fmaxf(M, s_mx[q][w]);
-        C += s_cs[q][w];
-      }
-      float sc = 1.f;  // s = 2^e with max/s <= 127
-      if (M > 0.f) {
-        int e;
-        frexpf(M / 127.f, &e);
-        sc = ldexpf(1.f, e);
-      }
-      inv[q] = 1.0 / (double)sc;
-      if (t == 0 && q < nk) {
-        st.fc[b].scale[k0 + q] = sc;
-        st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < MPT; ++c) {
-      const int j = t + c * NT;
-      if (j >= m) continue;
-      const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q >= nk) continue;
-        const int k = k0 + q;
-        const float wp = sgs[c] > 0.f ? W0[k * m + j] / sgs[c] : 0.f;
-        double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
-        int8_t dq[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const double r = rint(v);
-          dq[d] = (int8_t)r;
-          v = (v - r) * 128.0;
-        }
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-          dig[((((int64_t)ch * NB + (k >> 2)) * 64 + 16 * grp + 4 * (k & 3) + d) * 16) + jj] = (uint8_t)dq[d];
-      }
-    }
-    if (k0 + 4 < w0) __syncthreads();  // s_mx / s_cs are rewritten by the next pass
-  }
-}
+#include "update_core.h"
 
 // Per leapfrog step: ONE pass over the parameters computes the prior gradient,
 // the half-stepped momentum and every scalar of the step (log prior, kinetic

@@ -1,0 +1,389 @@
+// update_core.h — the register-resident leapfrog update of one small fused
+// branch (update_small) and its workgroup reductions, shared by the update
+// kernel (kernels_update.hip) and the gradient kernel's fused tail
+// (kernels_fx.hip: the last workgroup of a branch updates it in the same launch).
+#pragma once
+#include <math.h>
+
+#include "bann_internal.h"
+
+// NV doubles summed over the workgroup in one pass (one barrier pair)
+template <int NT, int NV>
+__device__ void block_sum_n(double (&v)[NV], double* red) {
+#pragma unroll
+  for (int q = 0; q < NV; ++q)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q * (NT / 64) + w] = v[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += red[q * (NT / 64) + k];
+    v[q] = t;
+  }
+}
+
+// Register-resident update of a fused branch (P <= UPD_CAP * NT, m <= MPT * NT, <= 4
+// first-layer columns, or a wide branch with <= 32: every C2/C3/C4/C5 branch).  All global loads of the
+// step are issued up front (partials, theta, lambda, momentum, eps, theta0,
+// mu, sigma), the parameters stay in registers between the reduction and the
+// position step, and the W0-digit refresh reads the new W0 from LDS: two
+// memory latencies and two workgroup reductions per launch instead of about
+// seven dependent global round trips (the launch follows a genotype stream that
+// has evicted all of it from L2).  Same arithmetic as the general path below.
+#define UPD_CAP 8
+// parameters per thread: the 512-thread kernel only takes P <= 2048 (update_is_large
+// sends the rest to the 1024-thread one), so 4 -- 20 fewer VGPRs, same bits
+template <int NT>
+constexpr int upd_cap() { return NT == 512 ? 4 : UPD_CAP; }
+// NV doubles summed over a VIRTUAL workgroup of NT * R threads run by NT threads
+// (replica r of thread t is virtual thread t + r NT): the reduction order of
+// block_sum_n<NT * R> exactly, so a fused update in a 256-thread gradient
+// workgroup gives the bits of the 512-thread update kernel
+template <int NT, int R, int NV>
+__device__ void block_sum_nv(double (&v)[R][NV], double* red) {
+  constexpr int NWV = NT * R / 64;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int q = 0; q < NV; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v[r][q] += __shfl_xor(v[r][q], o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int q = 0; q < NV; ++q) red[q * NWV + w + r * (NT / 64)] = v[r][q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double t = 0.0;
+    for (int k = 0; k < NWV; ++k) t += red[q * NWV + k];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r][q] = t;
+  }
+}
+
+// R > 1: NT real threads play a workgroup of NT * R (the fused update in the tail
+// of the fx gradient launch, bann_api.hip run_grad): every per-element operation,
+// every partial sum and both reductions in the order of update_small<NT * R>.
+template <int NT, int MPT, int R = 1>
+__device__ void update_small(const DevState& st, int b, const BranchDev& bd, int mode, bool prof, int step,
+                             double* redd, float* s_th) {
+  constexpr int NV_T = NT * R;  // the virtual workgroup
+  const int P = bd.P, m = bd.m, w0 = bd.widths[0];
+  const int64_t base = bd.p_off;
+  // a finished trajectory (STEP / LAST after an early rejection) is left alone; the
+  // status is checked after every load of the step has been issued, not before
+  const bool check = !prof && (mode == MODE_STEP || mode == MODE_LAST);
+  const int status = st.status[b];
+  // marker statistics for the refresh, prefetched
+  float mus[R][MPT], sgs[R][MPT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < MPT; ++c) {
+      const int j = threadIdx.x + r * NT + c * NV_T;
+      mus[r][c] = j < m ? st.mu[bd.mk_off + j] : 0.f;
+      sgs[r][c] = j < m ? st.sigma[bd.mk_off + j] : 0.f;
+    }
+  double rss = 0.0;
+  for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
+  const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
+  const bool lasso = (bd.prior == 2 || bd.prior == 3);
+  constexpr int CAP = upd_cap<NV_T>();
+  float th[R][CAP], gr[R][CAP], pm[R][CAP], ep[R][CAP], t0[R][CAP];
+  double sums[R][3];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = threadIdx.x + r * NT;
+    sums[r][0] = sums[r][1] = sums[r][2] = 0.0;
+#pragma unroll
+    for (int c = 0; c < CAP; ++c) {
+      const int i = t + c * NV_T;
+      th[r][c] = gr[r][c] = pm[r][c] = ep[r][c] = t0[r][c] = 0.f;
+      if (i >= P) continue;
+      float d = 0.f;
+      for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
+      th[r][c] = st.theta[base + i];
+      const float lm = st.lam[base + i];
+      const float ll = st.lamld[base + i];
+      pm[r][c] = st.mom[base + i];
+      ep[r][c] = st.eps[base + i];
+      if (mode == MODE_STEP || mode == MODE_LAST) t0[r][c] = st.theta0[base + i];
+      const float sgn = th[r][c] > 0.f ? 1.f : (th[r][c] < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
+      const float reg = lasso ? lm * sgn : lm * th[r][c];
+      gr[r][c] = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
+      sums[r][0] -= lasso ? (double)ll * fabs((double)th[r][c]) : 0.5 * (double)ll * (double)th[r][c] * (double)th[r][c];
+      if (mode == MODE_INIT) {
+        sums[r][1] += (double)pm[r][c] * (double)pm[r][c];
+      } else if (mode != MODE_GRAD) {  // second half step of this leapfrog step (momentum.rs:121-136)
+        pm[r][c] = pm[r][c] + ep[r][c] * 0.5f * gr[r][c];
+        sums[r][1] += (double)pm[r][c] * (double)pm[r][c];
+        sums[r][2] += ((double)th[r][c] - (double)t0[r][c]) * (double)pm[r][c];
+      }
+    }
+  }
+  if (check && status != ST_RUNNING) return;
+  if (!prof)
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < CAP; ++c) {
+        const int i = threadIdx.x + r * NT + c * NV_T;
+        if (i < P) st.grad[base + i] = gr[r][c];
+      }
+  const int t = threadIdx.x;
+  if (mode == MODE_GRAD) {
+    double v1[R][1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v1[r][0] = sums[r][0];
+    block_sum_nv<NT, R, 1>(v1, redd);
+    if (t == 0) {
+      st.ld_out[b] = v1[0][0] - (double)le * rss / 2.0;
+      st.rss_out[b] = rss;
+    }
+    return;
+  }
+  block_sum_nv<NT, R, 3>(sums, redd);
+  // + log_density_wrt_rss (100-102); network mode: the rss term is added once for the network by the host
+  const double ld = sums[0][0] - (st.netmode ? 0.0 : (double)le * rss / 2.0);
+  const double h = ld - 0.5 * sums[0][1];                   // -H (878-883)
+  const int stride = st.lint + 1;
+  // what happens to theta: 0 = position step, 1 = restore theta0, 2 = keep
+  int act = 0;
+  if (mode == MODE_INIT) {
+    if (t == 0) {
+      st.h0[b] = h;
+      st.htrace[(int64_t)b * stride] = h;
+      st.status[b] = ST_RUNNING;
+      st.uturn[b] = -1;
+      st.rss_out[b] = rss;
+      st.ld_out[b] = ld;
+    }
+  } else {
+    const double h0 = st.h0[b];
+    const bool diverged = !prof && !st.netmode && fabs(h - h0) > (double)st.max_dh;
+    if (!prof && t == 0) st.htrace[(int64_t)b * stride + step] = h;
+    if (diverged) {  // RejectedEarly (1264-1279)
+      act = 1;
+      if (t == 0) st.status[b] = ST_REJECTED_EARLY;
+    } else {
+      if (!prof && t == 0 && sums[0][2] < 0.0 && st.uturn[b] < 0) st.uturn[b] = step - 1;  // 1281-1284
+      if (mode == MODE_LAST && st.netmode) {  // network mode: the host decides for the network
+        act = 2;
+        if (t == 0) {
+          st.ld_out[b] = ld;
+          st.rss_out[b] = rss;
+        }
+      } else if (mode == MODE_LAST) {  // Metropolis (928-962)
+        const double log_acc = h - h0;
+        const double acc_p = log_acc >= 0.0 ? 1.0 : exp(log_acc);
+        const bool accept = (double)st.uacc[b] < acc_p;
+        act = accept ? 2 : 1;
+        if (t == 0) {
+          st.status[b] = accept ? ST_ACCEPTED : ST_REJECTED;
+          st.ld_out[b] = ld;
+          st.rss_out[b] = rss;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < CAP; ++c) {
+      const int i = t + r * NT + c * NV_T;
+      if (i >= P) continue;
+      float tn = th[r][c];
+      if (act == 0) {  // (next) first half step + position step (params.rs:728-738)
+        const float p = pm[r][c] + 0.5f * ep[r][c] * gr[r][c];
+        tn = th[r][c] + ep[r][c] * p;
+        if (prof) {
+          st.grad[base + i] = tn;  // same traffic, chain unchanged
+          tn = th[r][c];
+        } else {
+          st.mom[base + i] = p;
+          st.theta[base + i] = tn;
+          if (mode == MODE_INIT) st.theta0[base + i] = th[r][c];
+        }
+      } else {
+        if (mode != MODE_INIT && !prof) st.mom[base + i] = pm[r][c];  // the half-stepped momentum
+        if (act == 1) {
+          tn = t0[r][c];
+          st.theta[base + i] = tn;
+        }
+      }
+      s_th[i] = tn;
+    }
+  __syncthreads();
+  // ---- W0 digit refresh from the new W0 in LDS (the general refresh_fused_const),
+  // four columns per pass (wide branches: eight passes, digit image of 8 column blocks) ----
+  const float* W0 = s_th + bd.woff[0];
+  const float* b0 = s_th + bd.boff[0];
+  const int NB = bd.fused == 2 ? 8 : 1;
+  uint8_t* dig = const_cast<uint8_t*>(st.dig) + bd.dig_off;
+  __shared__ float s_mx[4][NV_T / 64];
+  __shared__ double s_cs[4][NV_T / 64];
+  const int wv = t >> 6;
+  if (R == 1 && NT == 1024 && NB == 8 && m <= 128) {
+    // wide branches (C5: m = 125, w0 = 32): the eight four-column passes run side by
+    // side -- thread t takes marker t & 127 of column quad t >> 7 (waves 2q, 2q + 1),
+    // one barrier instead of sixteen.  The lane -> marker map and the reduction order
+    // are those of the pass loop below, so every bit of the digits, scales and c0 is too.
+    const int j = t & 127, kq = t >> 7;
+    const bool on = j < m;
+    const float sg = on ? st.sigma[bd.mk_off + j] : 0.f;
+    const float mu = on ? st.mu[bd.mk_off + j] : 0.f;
+    float mx[4], wq[4];
+    double cs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = 4 * kq + q;
+      wq[q] = (on && k < w0 && sg > 0.f) ? W0[k * m + j] / sg : 0.f;
+      mx[q] = fmaxf(0.f, fabsf(wq[q]));
+      cs[q] = 0.0;
+      if (on && k < w0) cs[q] += (double)mu * (double)wq[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o));
+        cs[q] += __shfl_xor(cs[q], o);
+      }
+    __shared__ float s_mx8[NT / 64][4];
+    __shared__ double s_cs8[NT / 64][4];
+    if ((t & 63) == 0)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s_mx8[wv][q] = mx[q];
+        s_cs8[wv][q] = cs[q];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = 4 * kq + q;
+      // (+ the other waves' zeros, as the pass loop adds them)
+      const float M = fmaxf(fmaxf(s_mx8[2 * kq][q], s_mx8[2 * kq + 1][q]), 0.f);
+      const double C = (s_cs8[2 * kq][q] + s_cs8[2 * kq + 1][q]) + 0.0;
+      float sc = 1.f;  // s = 2^e with max/s <= 127
+      if (M > 0.f) {
+        int e;
+        frexpf(M / 127.f, &e);
+        sc = ldexpf(1.f, e);
+      }
+      if (j == 0 && k < w0) {
+        st.fc[b].scale[k] = sc;
+        st.fc[b].c0[k] = (float)((double)b0[k] - C);
+      }
+      if (on && k < w0) {
+        double v = (double)wq[q] * (1.0 / (double)sc);
+        const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const double r = rint(v);
+          dig[((((int64_t)ch * NB + kq) * 64 + 16 * grp + 4 * q + d) * 16) + jj] = (uint8_t)(int8_t)r;
+          v = (v - r) * 128.0;
+        }
+      }
+    }
+    return;
+  }
+  for (int k0 = 0; k0 < w0; k0 += 4) {
+    const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
+    float mx[R][4];
+    double cs[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        mx[r][q] = 0.f;
+        cs[r][q] = 0.0;
+      }
+#pragma unroll
+      for (int c = 0; c < MPT; ++c) {
+        const int j = t + r * NT + c * NV_T;
+        if (j >= m) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q < nk) {
+            const float wp = sgs[r][c] > 0.f ? W0[(k0 + q) * m + j] / sgs[r][c] : 0.f;
+            mx[r][q] = fmaxf(mx[r][q], fabsf(wp));
+            cs[r][q] += (double)mus[r][c] * (double)wp;
+          }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mx[r][q] = fmaxf(mx[r][q], __shfl_xor(mx[r][q], o));
+          cs[r][q] += __shfl_xor(cs[r][q], o);
+        }
+    }
+    if ((t & 63) == 0)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s_mx[q][wv + r * (NT / 64)] = mx[r][q];
+          s_cs[q][wv + r * (NT / 64)] = cs[r][q];
+        }
+    __syncthreads();
+    double inv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float M = s_mx[q][0];
+      double C = s_cs[q][0];
+      for (int w = 1; w < NV_T / 64; ++w) {
+        M = fmaxf(M, s_mx[q][w]);
+        C += s_cs[q][w];
+      }
+      float sc = 1.f;  // s = 2^e with max/s <= 127
+      if (M > 0.f) {
+        int e;
+        frexpf(M / 127.f, &e);
+        sc = ldexpf(1.f, e);
+      }
+      inv[q] = 1.0 / (double)sc;
+      if (t == 0 && q < nk) {
+        st.fc[b].scale[k0 + q] = sc;
+        st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < MPT; ++c) {
+        const int j = t + r * NT + c * NV_T;
+        if (j >= m) continue;
+        const int ch = j >> 6, grp = (j & 63) >> 4, jj = j & 15;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= nk) continue;
+          const int k = k0 + q;
+          const float wp = sgs[r][c] > 0.f ? W0[k * m + j] / sgs[r][c] : 0.f;
+          double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
+          int8_t dq[4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const double rr = rint(v);
+            dq[d] = (int8_t)rr;
+            v = (v - rr) * 128.0;
+          }
+#pragma unroll
+          for (int d = 0; d < 4; ++d)
+            dig[((((int64_t)ch * NB + (k >> 2)) * 64 + 16 * grp + 4 * (k & 3) + d) * 16) + jj] = (uint8_t)dq[d];
+        }
+      }
+    if (k0 + 4 < w0) __syncthreads();  // s_mx / s_cs are rewritten by the next pass
+  }
+}
+

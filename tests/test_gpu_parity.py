@@ -1044,3 +1044,37 @@ def test_forward_fi_matches_lds_forward(Ctx, n, monkeypatch):
                 assert norm_rel(preds[1][b], O.predict(s["branch"], X)) < 1e-5, b
         ctx.close()
     assert np.array_equal(preds[0], preds[1])
+
+
+def test_fused_update_session_bitwise(Ctx, monkeypatch):
+    """a one-round multi-split fx plan (the N = 8 shard's shape: here 70 branches
+    x 4 splits = 280 work items) runs the leapfrog update in the gradient
+    launch's tail (the last workgroup of each branch, update_small as 512 virtual
+    threads): the trajectory -- statuses, parameters, predictions -- has the bits
+    of the separate update launches (BANN_FUSE_UPDATE=0)."""
+    rng = np.random.default_rng(77)
+    n, nb, m = 2048, 70, 60
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = []
+    for b in range(nb):
+        specs.append(dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, [4, 4, 1])),
+                          y=rng.normal(size=n).astype(np.float32)))
+    outs = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
+        ctx = build_context(Ctx, g, specs)
+        res = []
+        for traj, (L, f) in enumerate([(5, 0.5), (3, 2.0), (8, 0.3)]):
+            ctx.leapfrog_begin(list(range(nb)), L, 10.0, "izmailov", f, seed=3 + traj)
+            ctx.leapfrog_steps(L)
+            st, acc = ctx.leapfrog_end()
+            res.append((st.copy(), acc, [ctx.get_params(b) for b in range(nb)], ctx.residual_delta()))
+        outs.append(res)
+        ctx.close()
+    for (s0, a0, p0, d0), (s1, a1, p1, d1) in zip(*outs):
+        assert np.array_equal(s0, s1) and a0 == a1
+        assert 0 < a1 < nb or a1 == nb   # something moved
+        for b in range(nb):
+            assert np.array_equal(p0[b], p1[b]), b
+        assert np.array_equal(d0, d1)
