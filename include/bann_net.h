@@ -79,7 +79,9 @@ typedef struct {
  * (1 gamma); unless fixed precisions, per layer l < L-1 the weight precisions
  * (one gamma per input node for ARD priors, else one) then the bias precision
  * (1 gamma), then the output-layer precision (1 gamma); the momentum (P
- * normals, param_vec order); the acceptance uniform (1 uniform); then, with
+ * normals, param_vec order -- only while a normal hook is installed: without
+ * one the momentum is drawn on the device, as the reference's ArrayFire randn
+ * does, from one 64-bit seed of the built-in generator); the acceptance uniform (1 uniform); then, with
  * sampled output bias, 1 gamma + 1 normal.  Random step sizes: P uniforms
  * (param_vec order) before the momentum.  Joint HMC instead: no Gibbs draws;
  * P + Q uniforms (step sizes, [param_vec | precision_vec]), P + Q normals

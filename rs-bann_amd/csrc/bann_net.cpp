@@ -14,6 +14,7 @@
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -803,11 +804,21 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
       eps = dr.eps.data();
       mode = BANN_STEP_INJECTED;
     }
-    dr.mom.resize(B.P);
-    for (auto& p : dr.mom) p = (float)draw_normal(t);
+    // sample_momentum (branch_sampler.rs:594-609) draws on the device in the reference
+    // (ArrayFire randn): so does the driver unless the caller replays a host stream
+    // (RNG hooks, the parity tests) -- then P normals from the hook, uploaded
+    const bool dev_mom = !t->hooks.normal;
+    uint64_t mseed = 0;
+    if (dev_mom) {
+      mseed = t->gen();
+    } else {
+      dr.mom.resize(B.P);
+      for (auto& p : dr.mom) p = (float)draw_normal(t);
+    }
     dr.u = (float)draw_uniform(t);
     CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
-                      cfg->hmc_step_size_factor, eps, dr.mom.data(), 0, &dr.u, &status, nullptr, nullptr, nullptr));
+                      cfg->hmc_step_size_factor, eps, dev_mom ? nullptr : dr.mom.data(), mseed, &dr.u, &status,
+                      nullptr, nullptr, nullptr));
   }
   if (traj && !gd && !gdj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
     std::string line;
@@ -889,10 +900,28 @@ int train_record(bann_net* t, int chain_ix, const bann_mcmc_cfg* cfg, const std:
 
 }  // namespace
 
+namespace {
+// the driver's one-branch trajectories are launch-latency-bound: replay each as one
+// captured HIP graph (bann_set_graph_replay) unless BANN_HMC_GRAPH=0; the
+// context's own setting (BANN_HMC_GRAPH=1, default off) is restored after training
+struct GraphReplayScope {
+  bann_ctx* ctx;
+  explicit GraphReplayScope(bann_ctx* c) : ctx(c) {
+    const char* e = std::getenv("BANN_HMC_GRAPH");
+    (void)bann_set_graph_replay(ctx, !e || std::atoi(e) != 0);
+  }
+  ~GraphReplayScope() {
+    const char* e = std::getenv("BANN_HMC_GRAPH");
+    (void)bann_set_graph_replay(ctx, e && std::atoi(e) != 0);
+  }
+};
+}  // namespace
+
 extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg, const char* outdir) {
   if (!t || !y || !cfg) return BANN_E_ARG;
   const std::string dir = outdir ? outdir : "";
   bool trace = false, traj = false;
+  GraphReplayScope graphs(t->ctx);
   int rc = train_begin(t, y, n, cfg, dir, trace, traj);
   if (rc) return rc;
   const int nb = (int)t->br.size();
@@ -918,6 +947,7 @@ extern "C" int bann_net_train_single_branch(bann_net* t, const float* y, int64_t
   if (!t || !y || !cfg) return BANN_E_ARG;
   const std::string dir = outdir ? outdir : "";
   bool trace = false, traj = false;
+  GraphReplayScope graphs(t->ctx);
   int rc = train_begin(t, y, n, cfg, dir, trace, traj);
   if (rc) return rc;
   Draws dr;

@@ -36,9 +36,14 @@ grad = [r for r in trace if "k_fused_grad" in r["Kernel_Name"]]
 big = max(int(r["Grid_Size_X"]) for r in grad)
 full = [r for r in grad if int(r["Grid_Size_X"]) == big]
 dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in full]
-upd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace
-       if "k_update" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == max(
-           int(x["Grid_Size_X"]) for x in trace if "k_update" in x["Kernel_Name"])]
+upd_rows = [x for x in trace if "k_update" in x["Kernel_Name"]]
+upd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in upd_rows
+       if int(r["Grid_Size_X"]) == max(int(x["Grid_Size_X"]) for x in upd_rows)] if upd_rows else []
+# every kernel of the timed trajectory (e.g. the network sampler's forward-only launch)
+per_kernel = {}
+for r in timed:
+    k = r["Kernel_Name"].split("(")[0]
+    per_kernel.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 
 
 def pmc_bytes(sub, counter, pick=statistics.median):
@@ -101,16 +106,24 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
     f.write("| kernel | launches (full branch set) | mean ms | median ms | min ms |\n|---|---|---|---|---|\n")
     f.write(f"| {full[0]['Kernel_Name']} | {len(dur)} | {statistics.mean(dur):.3f} | "
             f"{statistics.median(dur):.3f} | {min(dur):.3f} |\n")
-    f.write(f"| k_update (full set) | {len(upd)} | {statistics.mean(upd):.3f} | {statistics.median(upd):.3f} | "
-            f"{min(upd):.3f} |\n\n")
+    if upd:
+        f.write(f"| k_update (full set) | {len(upd)} | {statistics.mean(upd):.3f} | {statistics.median(upd):.3f} | "
+                f"{min(upd):.3f} |\n\n")
+    else:
+        f.write("\n(no separate update launches: the update runs in the gradient launch's tail)\n\n")
     if tgrad:
         f.write(f"**Timed trajectory** ({len(tgrad)} gradient launches, {len(tupd)} update launches, "
                 f"span {tspan:.3f} ms for {bench['steps']} steps = {tspan / bench['steps']:.4f} ms per step): "
                 f"gradient launch mean {statistics.mean(tgrad):.4f} ms (median {statistics.median(tgrad):.4f}), "
-                f"update mean {statistics.mean(tupd):.4f} ms; "
+                f"update mean {statistics.mean(tupd) if tupd else 0.0:.4f} ms; "
                 f"algorithmic bytes / mean gradient launch = "
                 f"{pmc['alg_bytes_per_launch'] / (statistics.mean(tgrad) * 1e-3) / 1e9:.0f} GB/s = "
                 f"{pmc['alg_bytes_per_launch'] / (statistics.mean(tgrad) * 1e-3) / 8e12:.3f} of 8 TB/s\n\n")
+    if per_kernel:
+        f.write("Every kernel of the timed trajectory:\n\n| kernel | launches | mean ms | total ms |\n|---|---|---|---|\n")
+        for k, v in sorted(per_kernel.items(), key=lambda kv: -sum(kv[1])):
+            f.write(f"| {k} | {len(v)} | {statistics.mean(v):.4f} | {sum(v):.3f} |\n")
+        f.write("\n")
     f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.4f} ms "
             f"({bench['roofline'].get('kernel_ms_source', '')}); back-to-back "
             f"{bench['roofline'].get('kernel_ms_back_to_back', float('nan')):.4f} ms\n\n")
