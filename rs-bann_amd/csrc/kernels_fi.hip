@@ -221,7 +221,7 @@ __device__ __forceinline__ void fi_advance(const DevState& st, const GradItem* i
 // ahead in three buffers at 2 waves per SIMD measured slower: 1.33 vs 1.21 ms at
 // C3).
 template <int NL, int ACT, int NSEG>
-__global__ void __launch_bounds__(64 * FI_WAVES, 3) k_forward_fi(DevState st, const GradItem* __restrict__ items,
+__global__ void __launch_bounds__(64 * FI_WAVES, NL <= 3 ? 3 : 2) k_forward_fi(DevState st, const GradItem* __restrict__ items,
                                                                  int nitems) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;

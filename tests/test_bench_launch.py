@@ -35,3 +35,22 @@ def test_bench_single_rank_runs_in_process():
     out, err = _run(["--gpus", "1", "--check-launch"])
     assert "launching" not in err
     assert out["n_gpus"] == 1 and out["ranks"] == [0] and out["shards"] == [[0, 1000]]
+
+
+def test_step_factor_rule():
+    """the Izmailov factor c fixes the trajectory length L eps (ridge_ard.rs:70-117):
+    below the L a line was tuned at, bench.py keeps the tuned step size
+    (c = c_ref L / L_ref), above it the tuned trajectory length (c = c_ref)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    f = bench.default_step_factor
+    assert f("c3", "branch", False, 20) == 1.0 and f("c3", "branch", False, 100) == 1.0
+    assert abs(f("c3", "branch", False, 10) - 0.5) < 1e-12
+    assert abs(f("c5", "branch", False, 10) - 0.05) < 1e-12 and abs(f("c5", "branch", False, 20) - 0.1) < 1e-12
+    assert abs(f("c5", "branch", True, 10) - 0.01) < 1e-12
+    assert abs(f("c3", "network", False, 20) - 0.11) < 1e-12 and abs(f("c3", "network", False, 10) - 0.055) < 1e-12
+    assert abs(f("c3def", "branch", False, 4) - 0.008) < 1e-12 and f("c3def", "branch", False, 20) == 0.02
+    # an untuned line: the branch sampler's factor, one tenth for the joint network state
+    assert abs(f("c2", "network", False, 20) - 0.1) < 1e-12

@@ -42,7 +42,7 @@ def test_counted_fxl_instantiations_do_not_spill(tmp_path):
 
 def test_production_kernels_carry_no_profiling_switches():
     """the ablation / stamp switches live in the profiling copy
-    (tools/profiling/kernels_fx_ablate.hip), not in the shipped kernels"""
+    (tools/archive/profiling/kernels_fx_ablate.hip), not in the shipped kernels"""
     for f in os.listdir(os.path.dirname(SRC)):
         if f.endswith((".hip", ".h", ".cpp")):
             txt = open(os.path.join(os.path.dirname(SRC), f)).read()
