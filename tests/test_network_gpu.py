@@ -197,3 +197,50 @@ def test_rccl_one_rank_communicator():
     assert np.array_equal(plain.exchange_residual(y), rccl.exchange_residual(y))
     plain.close()
     rccl.close()
+
+
+def _torch_rccl_worker(rank, port, out):
+    """torch's own RCCL process group (backend "nccl", as bench.py at N > 1) live in the
+    same process as the library's RCCL communicator"""
+    import torch
+    import torch.distributed as dist
+    from bann.distributed import comm_unique_id
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    t = torch.ones(8, device="cuda:0")
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+    rng, g, specs = _problem(seed=21)
+    n, L = g.shape[1], 4
+    y = rng.normal(size=n).astype(np.float32)
+    eps, mom = _draws(rng, specs, L)
+    res = []
+    for use_rccl in (False, True):
+        ctx = _context(g, specs, range(len(specs)))
+        if use_rccl:
+            ctx.comm_init_rccl(comm_unique_id(), 1, 0)
+            out["info"] = ctx.comm_info()
+        r = ctx.network_hmc_step(y, L, bias=0.0, lambda_e=1.0, eps=np.concatenate(eps),
+                                 momentum=np.concatenate(mom), u=0.5)
+        res.append((r["status"], r["trace"], [ctx.get_params(i) for i in range(len(specs))]))
+        ctx.close()
+    dist.all_reduce(t)   # torch's communicator still works after the library's
+    torch.cuda.synchronize()
+    out["torch_sum"] = float(t[0].item())
+    out["same"] = bool(res[0][0] == res[1][0] and np.array_equal(res[0][1], res[1][1]) and
+                       all(np.array_equal(a, b) for a, b in zip(res[0][2], res[1][2])))
+    dist.destroy_process_group()
+
+
+def test_library_rccl_beside_torch_rccl():
+    """bench.py at N > 1 runs torch.distributed over RCCL (backend "nccl") AND the
+    library's own RCCL communicator in every rank process: both initialise and
+    work side by side (one rank on the one GPU of the box)."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_torch_rccl_worker, args=(_free_port(), out), nprocs=1, join=True)
+    assert out["info"]["kind"] == "rccl" and out["info"]["backend_ranks"] == 1
+    assert out["same"] and out["torch_sum"] == 1.0
