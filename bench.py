@@ -241,10 +241,9 @@ def main():
                          "reference's own sweep order, one branch at a time against the refreshed residual "
                          "(bann_net_train, Net::train net.rs:201-358), one GPU")
     ap.add_argument("--no-network-check", action="store_true",
-                    help="N > 1: skip the untimed network-joint trajectory through the library's RCCL communicator "
-                         "that runs before the warmup and is reported in the line (network_check)")
-    ap.add_argument("--network-check", action="store_true",
-                    help="N = 1: run that check too, through a 1-rank RCCL communicator")
+                    help="skip the untimed network-joint trajectory through the library's RCCL communicator "
+                         "(a 1-rank one at N = 1) that runs before the warmup and is reported in the line "
+                         "(network_check)")
     ap.add_argument("--accept-trajectories", type=int, default=None,
                     help="untimed trajectories after the timed one whose acceptance is reported beside it "
                          "(default 4 for --sampler network: one Metropolis decision per trajectory)")
@@ -348,7 +347,7 @@ def main():
     def library_comm():
         """the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
         all-reduce callback when rehearsing N ranks on one GPU"""
-        if dist is None:   # one rank: a 1-rank RCCL communicator (--network-check)
+        if dist is None:   # one rank: a 1-rank RCCL communicator
             ctx.comm_init_rccl(comm_unique_id(), 1, 0)
         elif backend == "nccl":
             import torch
@@ -409,7 +408,7 @@ def main():
     # factor for its L.  A stalled collective ends the run with a non-zero exit
     # (watchdog), an error likewise; the line is never printed without it.
     netcheck = None
-    if args.sampler == "branch" and not args.no_network_check and (dist is not None or args.network_check):
+    if args.sampler == "branch" and not args.no_network_check:
         import threading
         wd = threading.Timer(180.0, lambda: (log(f"network_check: rank {rank}: collective stalled"), os._exit(3)))
         wd.daemon = True

@@ -21,12 +21,14 @@ shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
 trace = list(csv.DictReader(open(find("trace", "*kernel_trace.csv"))))
 bench = json.loads(open(os.path.join(out, "bench_trace.json")).read().strip().splitlines()[-1])
 
-# the timed trajectory: bench.py runs the warmup trajectory, then the back-to-back
-# measurement session (a 2-step leapfrog session), then the timed trajectory;
-# each starts with one k_step_sizes launch (traj_prepare)
+# the timed trajectory: bench.py runs the network check's trajectory (when the line
+# carries network_check), the warmup trajectory, then the back-to-back measurement
+# session (a 2-step leapfrog session), then the timed trajectory; each starts with
+# one k_step_sizes launch (traj_prepare)
 trace.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(trace) if "k_step_sizes" in r["Kernel_Name"]]
-timed = trace[starts[2]:starts[3] if len(starts) > 3 else len(trace)] if len(starts) > 2 else []
+t_ix = 2 + (1 if bench.get("network_check") else 0) - (0 if bench.get("warmup") else 1)
+timed = trace[starts[t_ix]:starts[t_ix + 1] if len(starts) > t_ix + 1 else len(trace)] if len(starts) > t_ix else []
 tgrad = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_fused_grad" in r["Kernel_Name"]]
 tupd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_update" in r["Kernel_Name"]]
 tspan = ((int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])) / 1e6) if timed else 0.0
