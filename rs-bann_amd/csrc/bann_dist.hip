@@ -219,6 +219,10 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   CK(hipMemcpyAsync(ctx->d_nety, y, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
   ctx->st.netmode = 1;
   ctx->st.net_le = lambda_e;
+  // fx-only plans: the gradient kernel reads e itself (DevState::nete), no per-branch targets
+  bool fx_only = p.gx.empty();
+  for (const auto& g : p.groups) fx_only = fx_only && g.kind == 1;
+  ctx->st.nete = fx_only ? ctx->d_netsum : nullptr;
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
   // (launch timing, when enabled: forward, all-reduce, gradient and update spans)
   auto forward_and_targets = [&](int k) -> int {
@@ -231,8 +235,8 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
     r = allreduce_device_f32(ctx, ctx->d_netsum, n);
     if (r) return r;
     tm_mark(ctx, TM_AR1);
-    launch_net_targets(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart, ctx->d_netrss + k,
-                       ctx->stream);
+    launch_net_targets(ctx->st, p.d_all, fx_only ? 0 : nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart,
+                       ctx->d_netrss + k, ctx->stream);
     tm_mark(ctx, TM_GRAD0);
     r = run_grad(ctx, p, 0);
     tm_mark(ctx, TM_GRAD1);
@@ -250,6 +254,7 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
     }
   }
   ctx->st.netmode = 0;
+  ctx->st.nete = nullptr;
   if (rc) {
     ctx->tm_marks.clear();
     return rc;

@@ -135,6 +135,8 @@ struct DevState {
   const float* ows;       // [nbranch][2]: output-weight summary stat of the OTHER branches (reg_sum), and
                           //   the network's output-weight count (OutputWeightSummaryStats, params.rs:404-465)
   int32_t netmode;        // network-joint HMC: no per-branch rss term / decisions in k_update
+  const float* nete;      // network mode: the network's output error e = sum f + bias - y [n], read by the
+                          //   fx gradient kernel as every branch's error (no per-branch targets); else null
   float net_le;           // its error precision (every branch's)
   float hyper[6];         // NetworkPrecisionHyperparameters: (shape, scale) dense, summary, output (params.rs:134-142)
 };

@@ -87,7 +87,9 @@ struct bann_ctx {
   int64_t xi_bytes = 0;
   int32_t cus = 256;
   int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
-  bool fuse_update_on = true;
+  // the update in the gradient launch's tail (BANN_FUSE_UPDATE=1): off by default -- at the
+  // N = 8 shard its agent-scope fences under the genotype stream cost 0.292 vs 0.204 ms per step
+  bool fuse_update_on = false;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;

@@ -201,7 +201,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   char* const sd = &s_dig[wave][0];
   char* const sd_w = sd + (i16 >> 2) * FX_DROW + (4 * g + (i16 & 3)) * 16;  // row K(iota)
   const char* const sd_r = sd + g * FX_DROW + tq * 16 + 8 * tp;
-  const float* ybr = st.y + bd.y_off;
+  // the tile's targets -- or, in network mode, the network's output error, the same
+  // n-vector for every branch (bann_network_hmc_step)
+  const bool net_err = st.nete != nullptr;
+  const float* ybr = net_err ? st.nete : st.y + bd.y_off;
   float* predb = st.pred + bd.y_off;
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       float out = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], Wh[NL - 1][j][0], out);
-      const float e = valid ? out - yv : 0.f;
+      const float e = valid ? (net_err ? yv : out - yv) : 0.f;
       if (write_pred && valid) predb[row] = out;
       rss += (double)e * (double)e;
       float err[4];
