@@ -213,16 +213,19 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     if (d.fused == 1) {  // fx: (L, act, exactly 8 chunks)
       key.L = h.L;
       key.full = d.nchunks == 8;
-    } else if (d.fused == 3) {  // fxl: (L, act, waves, every wave 8 chunks)
+    } else if (d.fused == 3) {  // fxl: (L, act, chunks per wave, waves, every wave full)
       key.L = h.L;
-      key.nw = (d.nchunks + 7) / 8;
-      key.full = d.nchunks == 8 * key.nw;
+      key.cpw = fxl_cpw(d.nchunks);
+      key.nw = (d.nchunks + key.cpw - 1) / key.cpw;
+      key.full = d.nchunks == key.cpw * key.nw;
     } else if (d.fused == 2) {  // wx: (act, marker chunks: the plane kernel is compiled per chunk count)
       key.nw = d.nchunks;
     }
     LaunchGroup* grp = nullptr;
     for (auto& g : p.groups)
-      if (g.kind == key.kind && g.L == key.L && g.act == key.act && g.nw == key.nw && g.full == key.full) grp = &g;
+      if (g.kind == key.kind && g.L == key.L && g.act == key.act && g.nw == key.nw && g.full == key.full &&
+          g.cpw == key.cpw)
+        grp = &g;
     if (!grp) {
       p.groups.push_back(key);
       grp = &p.groups.back();
@@ -254,7 +257,8 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
   }
   {  // the fused update (kernels_fx.hip tail): fx branches only, the small update, one round of items
     int64_t items = 0;
-    bool ok = !solo && p.gx.empty() && ctx->d_upd_cnt != nullptr && ctx->fuse_update_on;
+    bool ok = !solo && p.gx.empty() && ctx->d_upd_cnt != nullptr && ctx->fuse_update_mode > 0;
+    bool single = true;  // every branch one split: its one workgroup updates it
     for (const auto& g : p.groups) {
       ok = ok && g.kind == 1;
       items += (int64_t)g.items.size();
@@ -262,8 +266,9 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     for (int i = 0; i < nb && ok; ++i) {
       const BranchHost& h = ctx->br[branches[i]];
       ok = h.P <= 2048 && h.m <= 512 && !update_is_large(h.dev);
+      single = single && h.dev.nsplits == 1;
     }
-    p.fuse_update = ok && items > 0 && items <= 2ll * ctx->cus;
+    p.fuse_update = ok && items > 0 && (single || (ctx->fuse_update_mode > 1 && items <= 2ll * ctx->cus));
   }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
   std::stable_sort(p.gx.begin(), p.gx.end(),
@@ -371,7 +376,7 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode, int upd
     if (g.kind == 2)
       launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, wp, ctx->stream);
     else if (g.kind == 3)
-      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, wp, ctx->stream);
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, wp, ctx->stream);
     else
       launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, upd_mode, upd_step, cnt, ctx->stream);
   }
@@ -402,7 +407,7 @@ int run_forward(bann_ctx* ctx, const Plan& p) {
     if (g.kind == 2)
       launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, 1, ctx->stream);
     else if (g.kind == 3)
-      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.full, 1, ctx->stream);
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, 1, ctx->stream);
     else if (g.fi)
       launch_forward_fi(s, g.d_items, ni, g.tiles, g.L, g.act, g.max_seg, ctx->cus, ctx->stream);
     else
@@ -461,7 +466,7 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   bann_ctx* ctx = new bann_ctx();
   ctx->device = device;
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
-  if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_on = atoi(e) != 0;
+  if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 2 : 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return BANN_E_HIP;
@@ -788,10 +793,19 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     return best_sp;
   };
   const bool env_split = getenv("BANN_TARGET_ITEMS") || getenv("BANN_MIN_FRAGS");
-  int64_t nfx = 0, nfxl[9] = {};
+  int64_t nfx = 0, nfxl[2][9] = {};  // fxl branches by (chunks per wave 4?, waves)
+  auto fxl_key = [](int nch, int& c4, int& nw) {
+    const int cpw = fxl_cpw(nch);
+    c4 = cpw == 4;
+    nw = (nch + cpw - 1) / cpw;
+  };
   for (auto& h : ctx->br) {
     if (h.dev.fused == 1) ++nfx;
-    if (h.dev.fused == 3) ++nfxl[(h.dev.nchunks + 7) / 8];
+    if (h.dev.fused == 3) {
+      int c4, nw;
+      fxl_key(h.dev.nchunks, c4, nw);
+      ++nfxl[c4][nw];
+    }
   }
   const int32_t fx_splits = best_splits(nfx, 2 * (int64_t)cus, 4);  // fx: 2 workgroups of 4 waves per CU, tiles interleaved
   int64_t nwx = 0;
@@ -799,11 +813,13 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   // wx: 4 two-wave workgroups per CU, a tile at a time (exact f32 MFMA); wx3: 2
   // four-wave workgroups per CU, two tiles at a time
   const int32_t wx_splits = wx_exact() ? best_splits(nwx, 4 * (int64_t)cus, 1) : best_splits(nwx, 2 * (int64_t)cus, 2);
-  int32_t fxl_splits[9] = {};
-  for (int nw = 2; nw <= 8; ++nw) {  // fxl: all waves of a workgroup on one tile; LDS- and VGPR-limited residency
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4), 8 / nw));
-    fxl_splits[nw] = best_splits(nfxl[nw], per_cu * cus, 1);
-  }
+  int32_t fxl_splits[2][9] = {};
+  for (int c4 = 0; c4 < 2; ++c4)
+    for (int nw = 1; nw <= 8; ++nw) {  // fxl: all waves of a workgroup on one tile; LDS- and VGPR-limited residency
+      const int64_t per_cu =
+          std::max<int64_t>(1, std::min<int64_t>(163840 / fxl_lds_bytes(nw, 4, c4 ? 4 : 8), 8 / nw));
+      fxl_splits[c4][nw] = best_splits(nfxl[c4][nw], per_cu * cus, 1);
+    }
   int64_t q_off = 0;
   // forward-only fi images (kernels_fi.hip) for the fx branches; BANN_FWD_FI=0: the LDS forward
   const bool fi_on = !(getenv("BANN_FWD_FI") && atoi(getenv("BANN_FWD_FI")) == 0);
@@ -857,7 +873,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     d.nsplits = d.fused ? (int32_t)std::max<int64_t>(1, (ctx->nfrag + frags_per_item - 1) / frags_per_item)
                         : (int32_t)((ntile + 63) / 64);
     if (d.fused == 1 && !env_split) d.nsplits = fx_splits;
-    if (d.fused == 3) d.nsplits = fxl_splits[(d.nchunks + 7) / 8];
+    if (d.fused == 3) {
+      int c4, nw;
+      fxl_key(d.nchunks, c4, nw);
+      d.nsplits = fxl_splits[c4][nw];
+    }
     if (d.fused == 2) d.nsplits = wx_splits;
     if (d.fused == 1)  // overflow guard also under the env overrides
       d.nsplits = std::max<int32_t>(d.nsplits, (int32_t)((ntile + 4 * BANN_MAX_TILES_PER_WAVE - 1) /

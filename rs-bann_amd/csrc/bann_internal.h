@@ -209,8 +209,9 @@ void launch_forward_fi(const DevState& st, const GradItem* items, int32_t nitems
 void launch_pack_fi(const uint8_t* raw, int64_t rowb, const PackJob* jobs, int32_t njobs, const int32_t* idx,
                     int64_t ntile, uint8_t* dst, hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                           int32_t nw, int full, int write_pred, hipStream_t s);
-int fxl_lds_bytes(int nw, int nl);
+                           int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s);
+int fxl_lds_bytes(int nw, int nl, int cpw);
+int fxl_cpw(int nchunks);  // marker chunks per fxl wave: 4 up to 32 chunks, else 8
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,
                        int izmailov, float c, int32_t L, hipStream_t s);
 void launch_restore_pred(const DevState& st, const int32_t* branches, int32_t nb, hipStream_t s);

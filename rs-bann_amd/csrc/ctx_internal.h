@@ -27,6 +27,7 @@ struct BranchHost {
 struct LaunchGroup {
   int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
   int32_t L = 0, act = 0, nw = 1, full = 0;
+  int32_t cpw = 8;      // fxl: marker chunks per wave (fxl_cpw)
   int64_t tiles = 0;    // fx: the items' 64-individual tiles (the fi forward's index space, GradItem::tile0)
   int32_t max_seg = 1;  // fx: the largest 256-marker segment count of its branches
   bool fi = false;      // fx: every branch has an individual-major fi image (kernels_fi.hip)
@@ -87,9 +88,11 @@ struct bann_ctx {
   int64_t xi_bytes = 0;
   int32_t cus = 256;
   int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
-  // the update in the gradient launch's tail (BANN_FUSE_UPDATE=1): off by default -- at the
-  // N = 8 shard its agent-scope fences under the genotype stream cost 0.292 vs 0.204 ms per step
-  bool fuse_update_on = false;
+  // the update in the gradient launch's tail: 1 (default) = plans whose branches have one
+  // split each (the workgroup that computed a branch's gradient updates it: no counter, no
+  // fence); 2 (BANN_FUSE_UPDATE=1) = also one-round multi-split plans (last arriver, agent
+  // fences: at the N = 8 shard 0.292 vs 0.204 ms per step, so not by default); 0 = never
+  int fuse_update_mode = 1;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;

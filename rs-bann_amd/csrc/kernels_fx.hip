@@ -546,15 +546,20 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // update kernel's arithmetic and reduction order (update_small as 512 virtual
     // threads), instead of a second launch.  Release the partials, count the
     // arrival, acquire the other workgroups' partials.
+    // A branch of one split has one workgroup: this one, whose partial slab is
+    // visible to its own waves after a workgroup barrier (no counter, no fence).
     __shared__ int s_last;
     __shared__ double s_redd[4 * 8];
-    __threadfence();
+    const bool single = bd.nsplits == 1;
+    if (!single) __threadfence();
     __syncthreads();
-    if (threadIdx.x == 0) s_last = atomicAdd(&upd_cnt[b], 1) == bd.nsplits - 1;
+    if (threadIdx.x == 0) s_last = single || atomicAdd(&upd_cnt[b], 1) == bd.nsplits - 1;
     __syncthreads();
     if (s_last) {
-      __threadfence();
-      if (threadIdx.x == 0) upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
+      if (!single) {
+        __threadfence();
+        if (threadIdx.x == 0) upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
+      }
       float* s_th = reinterpret_cast<float*>(&s_x[0][0][0]);  // the tile slots are free: P <= 2048 floats
       update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
     }
@@ -836,25 +841,34 @@ __device__ __forceinline__ void vm_wait_tie(int k, v4i& d) {
   }
 }
 
-int fxl_lds_bytes(int nw, int nl) {
+int fxl_lds_bytes(int nw, int nl, int cpw) {
   const int ns = 8 + (nl - 2) * 20;
-  return nw * (2 * FX_SLOT + 4 * FX_DROW + 2 * 64 * 16) + 2 * 64 * 4 + nl * 20 * 4 + ns * 4;
+  return nw * (2 * cpw * 1024 + 4 * FX_DROW + 2 * 64 * 16) + 2 * 64 * 4 + nl * 20 * 4 + ns * 4;
 }
 
-template <int NL, int ACT, int FULL>
+// CPW: chunks per wave.  8 (branches of 33 .. 64 chunks): the wave's W0 digit
+// operand is read from L2 two chunks ahead of its MFMAs, every tile.  4 (<= 32
+// chunks, e.g. C2's 2 000 markers on 8 waves): the wave's four digit operands stay
+// in registers for the whole item (16 VGPRs; its dW0 digit sums take 64): no digit
+// traffic and no digit-load latency in the tile loop, half the per-wave work per
+// tile at the same 8 waves per CU.
+template <int NL, int ACT, int FULL, int CPW>
 __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     k_fused_grad_fxl(DevState st, const GradItem* __restrict__ items, int write_pred) {
   // Counted digit loads only where the kernel fits in 256 VGPRs without spills
-  // (every wave 8 chunks, <= 3 layers: C2's shape): a spill of a register whose
-  // load is still in flight would store garbage.  Elsewhere the digit loads are
-  // ordinary loads under the compiler's own (conservative) waits.
-  constexpr bool CNT = FULL && NL <= 3;
+  // (every wave 8 chunks, <= 3 layers: C2's shape before CPW = 4): a spill of a
+  // register whose load is still in flight would store garbage.  Elsewhere the
+  // digit loads are ordinary loads under the compiler's own (conservative) waits.
+  constexpr bool RES = CPW == 4;  // digit operands resident in registers
+  constexpr bool CNT = FULL && NL <= 3 && !RES;
+  constexpr int NWIN = 4 * CPW;   // 16-marker windows per wave
   constexpr int NH = NL - 1;
   constexpr int NS = 8 + (NH - 1) * 20;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int NW = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
-  char* const s_x = lds;                                                    // [NW][2][FX_SLOT]
-  char* const s_dig = s_x + NW * 2 * FX_SLOT;                               // [NW][4 * FX_DROW]
+  constexpr int SLOT = CPW * 1024;
+  char* const s_x = lds;                                                    // [NW][2][SLOT]
+  char* const s_dig = s_x + NW * 2 * SLOT;                                  // [NW][4 * FX_DROW]
   v4f* const s_xch = reinterpret_cast<v4f*>(s_dig + NW * 4 * FX_DROW);      // [2][NW][64]
   float* const s_y = reinterpret_cast<float*>(s_xch + 2 * NW * 64);         // [2][64]
   float* const s_hw = s_y + 128;                                            // [NL][20]
@@ -866,9 +880,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int nch = bd.nchunks;
-  const int cpw = FULL ? 8 : (nch + NW - 1) / NW;
+  const int cpw = FULL ? CPW : (nch + NW - 1) / NW;
   const int c0 = wave * cpw;
-  const int cw = FULL ? 8 : (nch - c0 < cpw ? nch - c0 : cpw);  // >= 1 (NW = ceil(nch / 8))
+  const int cw = FULL ? CPW : (nch - c0 < cpw ? nch - c0 : cpw);  // >= 1 (NW = ceil(nch / CPW))
   const int64_t n = st.n;
   const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
 
@@ -919,10 +933,10 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   const int64_t tile_bytes = (int64_t)nch * 1024;
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + (int64_t)c0 * 1024 + lane * 16;
   const char* dsrc = reinterpret_cast<const char*>(st.dig) + bd.dig_off + (int64_t)c0 * 1024 + lane * 16;
-  char* const xslot0 = s_x + wave * 2 * FX_SLOT;
+  char* const xslot0 = s_x + wave * 2 * SLOT;
 
   auto issue_chunk = [&](int tt, int sl, int c) {
-    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, xslot0 + sl * FX_SLOT + c * 1024);
+    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, xslot0 + sl * SLOT + c * 1024);
   };
   auto issue_y = [&](int tt, int sl) {  // wave 0 streams the tile's targets for every wave
     if (wave != 0) return;
@@ -930,9 +944,9 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     glds4(ybr + (row < n ? row : n - 1), s_y + sl * 64);
   };
 
-  v4i acc[32];
+  v4i acc[NWIN];
 #pragma unroll
-  for (int u = 0; u < 32; ++u) acc[u] = v4i{0, 0, 0, 0};
+  for (int u = 0; u < NWIN; ++u) acc[u] = v4i{0, 0, 0, 0};
   int R[4] = {0, 0, 0, 0};
   double rss = 0.0;
   float db[NH][4], dWo[4];
@@ -949,34 +963,54 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   }
 
   int tt = tb, sl = 0, xb = 0;
-  if (tt < te) {
-    for (int c = 0; c < cw; ++c) issue_chunk(tt, 0, c);
-    issue_y(tt, 0);
-  }
   auto ldig = [&](int off) -> v4i {
     if constexpr (CNT) return ld_counted(dsrc + off);
     return *reinterpret_cast<const v4i*>(dsrc + off);
   };
-  v4i Dn0 = ldig(0), Dn1 = Dn0;
-  if (FULL || cw > 1) Dn1 = ldig(1024);
+  v4i Dres[RES ? CPW : 1];  // RES: the wave's digit operands for the whole item
+  if constexpr (RES) {
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) Dres[c] = (FULL || c < cw) ? ldig(c * 1024) : v4i{0, 0, 0, 0};
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) asm volatile("" : "+v"(Dres[c]));  // landed: no compiler waits in the loop
+  }
+  if (tt < te) {
+    for (int c = 0; c < cw; ++c) issue_chunk(tt, 0, c);
+    issue_y(tt, 0);
+  }
+  v4i Dn0 = Dres[0], Dn1 = Dres[0];
+  if constexpr (!RES) {
+    Dn0 = ldig(0);
+    Dn1 = Dn0;
+    if (FULL || cw > 1) Dn1 = ldig(1024);
+  }
   for (; tt < te; ++tt, sl ^= 1, xb ^= 1) {
     const bool more = tt + 1 < te;
     // this tile's genotype block (and targets) have landed; the two digit loads may fly
-    vm_wait((FULL || cw > 1) ? 2 : 1);
-    const char* xs = xslot0 + sl * FX_SLOT;
+    if constexpr (RES)
+      vm_wait(0);
+    else
+      vm_wait((FULL || cw > 1) ? 2 : 1);
+    const char* xs = xslot0 + sl * SLOT;
 
     // ---- forward: partial Z0 over this wave's block ----
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
     {
-      v4i Dg[8];
-      Dg[0] = Dn0;
-      Dg[1] = Dn1;
+      v4i Dg[CPW];
+      if constexpr (RES) {
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) Dg[c] = Dres[c];
+      } else {
+        Dg[0] = Dn0;
+        Dg[1] = Dn1;
+      }
       v4u Xc = (v4u)lds_tr8_pair(xs + fo0, xs + fo1);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < CPW; ++c) {
         if (!FULL && c >= cw) continue;
         v4u Xn = Xc;
-        if (c + 1 < 8 && (FULL || c + 1 < cw))
+        if (c + 1 < CPW && (FULL || c + 1 < cw))
           Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
         if constexpr (CNT) {
           // loads younger than digit load c (issue order below: D(c+2) then
@@ -986,11 +1020,11 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
           constexpr int young_c[8] = {1, 2, 3, 3, 3, 3, 3, 2};
           vm_wait_tie(young_c[c], Dg[c]);
         }
-        if (c + 2 < 8 && (FULL || c + 2 < cw)) Dg[c + 2] = ldig((c + 2) * 1024);
+        if (!RES && c + 2 < CPW && (FULL || c + 2 < cw)) Dg[c + 2] = ldig((c + 2) * 1024);
         if (more)
           issue_chunk(tt + 1, sl ^ 1, c);
         else if (CNT)  // last tile: a harmless L2-resident DMA keeps the counts fixed
-          glds16(dsrc + c * 1024, xslot0 + (sl ^ 1) * FX_SLOT + c * 1024);
+          glds16(dsrc + c * 1024, xslot0 + (sl ^ 1) * SLOT + c * 1024);
         const v4i B0 = (v4i)(Xc & 0x03030303u);
         const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
         const v4i B2 = (v4i)(Xc & 0x30303030u);
@@ -1118,7 +1152,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     if (grow) {
       const int sh = g == 0 ? dl[0] : g == 1 ? dl[1] : g == 2 ? dl[2] : dl[3];
 #pragma unroll
-      for (int u = 0; u < 32; ++u)
+      for (int u = 0; u < NWIN; ++u)
         if (FULL || u < 4 * cw) acc[u] = shr_digits(acc[u], sh);
     }
     v4u w;
@@ -1132,7 +1166,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     // ---- backward: dW0 digit sums of this wave's block += G^T delta0 ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
-      constexpr int PD = FXL_PD;
+      constexpr int PD = FXL_PD < NWIN ? FXL_PD : NWIN;
       uint32_t wq[PD];
 #pragma unroll
       for (int u = 0; u < PD; ++u)
@@ -1143,17 +1177,17 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
       };
       v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);  // two windows ahead of their MFMA (as in fx)
 #pragma unroll
-      for (int u = 0; u < 32; ++u) {
+      for (int u = 0; u < NWIN; ++u) {
         if (!FULL && u >= 4 * cw) continue;
         const v4i Bv = Bn;
         Bn = Bn2;
-        if (u + 2 < 32 && (FULL || u + 2 < 4 * cw)) Bn2 = unpack(wq[(u + 2) % PD]);
-        if (u + PD < 32 && (FULL || u + PD < 4 * cw))
+        if (u + 2 < NWIN && (FULL || u + 2 < 4 * cw)) Bn2 = unpack(wq[(u + 2) % PD]);
+        if (u + PD < NWIN && (FULL || u + PD < 4 * cw))
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
         acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         // the next tile's first two digit operands, half a backward ahead of their use
-        if (u == FXL_DPRE && more) {
+        if (!RES && u == FXL_DPRE && more) {
           Dn0 = ldig(0);
           if (FULL || cw > 1) Dn1 = ldig(1024);
         }
@@ -1214,7 +1248,7 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
     const float dbc = g == 0 ? db0[0] : g == 1 ? db0[1] : g == 2 ? db0[2] : db0[3];
     const int m = bd.m;
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
+    for (int u = 0; u < NWIN; ++u) {
       if (!FULL && u >= 4 * cw) continue;
       const int mk = 16 * (4 * c0 + u) + i16;
       if (mk < m && g < bd.widths[0]) {
@@ -1226,20 +1260,20 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
   }
 }
 
-template <int NL, int FULL>
+template <int NL, int FULL, int CPW>
 static void launch_fxl_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nw, int wp,
                           hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * nw);
-  const size_t shm = (size_t)fxl_lds_bytes(nw, NL);
+  const size_t shm = (size_t)fxl_lds_bytes(nw, NL, CPW);
 #define FXL_GO(A)                                                                                      \
   do {                                                                                                 \
     static bool attr_ = false;                                                                         \
     if (!attr_) {                                                                                      \
-      (void)hipFuncSetAttribute((const void*)k_fused_grad_fxl<NL, A, FULL>,                            \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, fxl_lds_bytes(FXL_MAXW, 4)); \
+      (void)hipFuncSetAttribute((const void*)k_fused_grad_fxl<NL, A, FULL, CPW>,                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, fxl_lds_bytes(FXL_MAXW, 4, CPW)); \
       attr_ = true;                                                                                    \
     }                                                                                                  \
-    hipLaunchKernelGGL((k_fused_grad_fxl<NL, A, FULL>), grid, block, shm, s, st, items, wp);           \
+    hipLaunchKernelGGL((k_fused_grad_fxl<NL, A, FULL, CPW>), grid, block, shm, s, st, items, wp);      \
   } while (0)
   switch (act) {
     case 0: FXL_GO(0); break;
@@ -1251,18 +1285,29 @@ static void launch_fxl_nl(const DevState& st, const GradItem* items, int32_t nit
 #undef FXL_GO
 }
 
-// nw waves per workgroup (= ceil(chunks / 8) of every branch of the launch);
-// full: every branch has exactly 8 * nw chunks
+int fxl_cpw(int nchunks) {
+  static const int force = getenv("BANN_FXL_CPW") ? atoi(getenv("BANN_FXL_CPW")) : 0;  // 8: the old scheme (A/B)
+  return (nchunks <= 4 * FXL_MAXW && force != 8) ? 4 : 8;
+}
+
+// nw waves per workgroup (= ceil(chunks / cpw) of every branch of the launch);
+// full: every branch has exactly cpw * nw chunks
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                           int32_t nw, int full, int write_pred, hipStream_t s) {
-  if (nitems <= 0 || nw < 1 || nw > FXL_MAXW) return;
-  switch (L * 2 + (full ? 1 : 0)) {
-    case 4: launch_fxl_nl<2, 0>(st, items, nitems, act, nw, write_pred, s); break;
-    case 5: launch_fxl_nl<2, 1>(st, items, nitems, act, nw, write_pred, s); break;
-    case 6: launch_fxl_nl<3, 0>(st, items, nitems, act, nw, write_pred, s); break;
-    case 7: launch_fxl_nl<3, 1>(st, items, nitems, act, nw, write_pred, s); break;
-    case 8: launch_fxl_nl<4, 0>(st, items, nitems, act, nw, write_pred, s); break;
-    case 9: launch_fxl_nl<4, 1>(st, items, nitems, act, nw, write_pred, s); break;
+                           int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s) {
+  if (nitems <= 0 || nw < 1 || nw > FXL_MAXW || (cpw != 4 && cpw != 8)) return;
+  switch (L * 4 + (full ? 2 : 0) + (cpw == 4 ? 1 : 0)) {
+    case 8: launch_fxl_nl<2, 0, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 9: launch_fxl_nl<2, 0, 4>(st, items, nitems, act, nw, write_pred, s); break;
+    case 10: launch_fxl_nl<2, 1, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 11: launch_fxl_nl<2, 1, 4>(st, items, nitems, act, nw, write_pred, s); break;
+    case 12: launch_fxl_nl<3, 0, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 13: launch_fxl_nl<3, 0, 4>(st, items, nitems, act, nw, write_pred, s); break;
+    case 14: launch_fxl_nl<3, 1, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 15: launch_fxl_nl<3, 1, 4>(st, items, nitems, act, nw, write_pred, s); break;
+    case 16: launch_fxl_nl<4, 0, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 17: launch_fxl_nl<4, 0, 4>(st, items, nitems, act, nw, write_pred, s); break;
+    case 18: launch_fxl_nl<4, 1, 8>(st, items, nitems, act, nw, write_pred, s); break;
+    case 19: launch_fxl_nl<4, 1, 4>(st, items, nitems, act, nw, write_pred, s); break;
     default: break;
   }
 }

@@ -31,9 +31,13 @@ def test_counted_fxl_instantiations_do_not_spill(tmp_path):
         m = re.search(r"VGPRs Spill: (\d+)", line)
         if m and name:
             spills[name] = int(m.group(1))
-    counted = [k for k in spills if re.match(r"_Z16k_fused_grad_fxlILi[23]ELi\dELi1E", k)]
+    counted = [k for k in spills if re.match(r"_Z16k_fused_grad_fxlILi[23]ELi\dELi1ELi8E", k)]
     assert len(counted) == 10, counted
     assert all(spills[k] == 0 for k in counted), {k: spills[k] for k in counted}
+    # 4 chunks per wave: the digit operands stay in registers for the whole item
+    resident = [k for k in spills if re.match(r"_Z16k_fused_grad_fxlILi[23]ELi\dELi[01]ELi4E", k)]
+    assert len(resident) == 20, resident
+    assert all(spills[k] == 0 for k in resident), {k: spills[k] for k in resident}
     fx = [k for k in spills if k.startswith("_Z15k_fused_grad_fx")]
     assert fx and all(spills[k] == 0 for k in fx), {k: spills[k] for k in fx}
     fwd = [k for k in spills if k.startswith("_Z12k_forward_fx")]

@@ -1046,14 +1046,18 @@ def test_forward_fi_matches_lds_forward(Ctx, n, monkeypatch):
     assert np.array_equal(preds[0], preds[1])
 
 
-def test_fused_update_session_bitwise(Ctx, monkeypatch):
-    """a one-round multi-split fx plan (the N = 8 shard's shape: here 70 branches
-    x 4 splits = 280 work items) runs the leapfrog update in the gradient
-    launch's tail (the last workgroup of each branch, update_small as 512 virtual
-    threads): the trajectory -- statuses, parameters, predictions -- has the bits
-    of the separate update launches (BANN_FUSE_UPDATE=0)."""
+@pytest.mark.parametrize("shape,fused", [("multi", "1"), ("single", None)])
+def test_fused_update_session_bitwise(Ctx, monkeypatch, shape, fused):
+    """the leapfrog update in the gradient launch's tail (update_small as 512
+    virtual threads) gives the bits of the separate update launches
+    (BANN_FUSE_UPDATE=0): statuses, parameters, predictions.
+      multi: a one-round multi-split fx plan (the N = 8 shard's shape: here 70
+        branches x 7 splits), the last arriving workgroup of each branch updates
+        it (BANN_FUSE_UPDATE=1);
+      single: one split per branch (C3's shape: 600 branches on 2 048
+        individuals), each branch's one workgroup updates it (the default)."""
     rng = np.random.default_rng(77)
-    n, nb, m = 2048, 70, 60
+    n, nb, m = (2048, 70, 60) if shape == "multi" else (1024, 600, 20)
     g = O.synthetic_genotypes(rng, n, nb * m)
     specs = []
     for b in range(nb):
@@ -1061,9 +1065,12 @@ def test_fused_update_session_bitwise(Ctx, monkeypatch):
                           branch=f32_branch(O.random_branch(rng, m, [4, 4, 1])),
                           y=rng.normal(size=n).astype(np.float32)))
     outs = []
-    for fuse in ("0", "1"):
-        monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
-        ctx = build_context(Ctx, g, specs)
+    for fuse in ("0", fused):
+        if fuse is None:
+            monkeypatch.delenv("BANN_FUSE_UPDATE", raising=False)
+        else:
+            monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
+        ctx = build_context(Ctx, g, specs)   # single: 600 branches -> 1 split each (bann_api.hip best_splits)
         res = []
         for traj, (L, f) in enumerate([(5, 0.05), (3, 2.0), (8, 0.02)]):
             ctx.leapfrog_begin(list(range(nb)), L, 10.0, "izmailov", f, seed=3 + traj)

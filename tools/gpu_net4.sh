@@ -14,3 +14,14 @@ for f in ${C5F:-0.002 0.005}; do
   timeout -k 10 400 python bench.py --config c5 --sampler network --step-factor $f --steps 20 --warmup 0 --accept-trajectories 2 --no-cpu-baseline > $OUT/c5net_$f.json 2> $OUT/c5net_$f.err || { tail $OUT/c5net_$f.err; exit 1; }
   j $OUT/c5net_$f.json
 done
+# C3 branch sampler: the update in the gradient launch's tail (default for one-split plans) vs its own launch
+for v in def 0 def 0; do
+  if [ $v = def ]; then E="env -u BANN_FUSE_UPDATE"; else E="env BANN_FUSE_UPDATE=0"; fi
+  $E timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/c3_fuse$v.json 2> $OUT/c3_fuse$v.err || { tail $OUT/c3_fuse$v.err; exit 1; }
+  j $OUT/c3_fuse$v.json
+done
+# C2: fxl with 4 chunks per wave and resident digit operands (default) vs 8 chunks per wave (BANN_FXL_CPW=8)
+for v in 4 8 4; do
+  BANN_FXL_CPW=$v timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu-baseline --no-network-check > $OUT/c2_cpw$v.json 2> $OUT/c2_cpw$v.err || { tail $OUT/c2_cpw$v.err; exit 1; }
+  j $OUT/c2_cpw$v.json
+done
