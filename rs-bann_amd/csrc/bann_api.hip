@@ -247,6 +247,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       grp->tiles += ((it.frag_end + 3) >> 2) - (it.frag_begin >> 2);
       it.part_at = solo ? solo_part + (int64_t)s * spi * h.P : d.part_off + (int64_t)s * spi * h.P;
       it.rss_at = solo ? solo_rss + (int64_t)s * spi : (int64_t)b * ctx->max_splits + (int64_t)s * spi;
+      it.fold_ix = solo ? (int32_t)p.fold.size() : -1;  // this branch's job, pushed below
       grp->items.push_back(it);
     }
     if (solo) {
@@ -257,7 +258,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
   }
   {  // the fused update (kernels_fx.hip tail): fx branches only, the small update, one round of items
     int64_t items = 0;
-    bool ok = !solo && p.gx.empty() && ctx->d_upd_cnt != nullptr && ctx->fuse_update_mode > 0;
+    bool ok = p.gx.empty() && ctx->d_upd_cnt != nullptr && ctx->fuse_update_mode > 0;
     bool single = true;  // every branch one split: its one workgroup updates it
     for (const auto& g : p.groups) {
       ok = ok && g.kind == 1;
@@ -268,7 +269,8 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       ok = h.P <= 2048 && h.m <= 512 && !update_is_large(h.dev);
       single = single && h.dev.nsplits == 1;
     }
-    p.fuse_update = ok && items > 0 && (single || (ctx->fuse_update_mode > 1 && items <= 2ll * ctx->cus));
+    // solo plans: the last arriving workgroup folds the branch's slabs, then updates it
+    p.fuse_update = ok && items > 0 && (solo || single || (ctx->fuse_update_mode > 1 && items <= 2ll * ctx->cus));
   }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
   std::stable_sort(p.gx.begin(), p.gx.end(),
@@ -371,6 +373,8 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode, int upd
   if (write_pred == 2) s.pred = ctx->d_pred0;
   const int wp = write_pred != 0;
   int32_t* cnt = upd_mode >= 0 ? ctx->d_upd_cnt : nullptr;
+  // a fused solo plan folds in the gradient launch's tail (kernels_fx.hip), not in k_fold_solo
+  const FoldJob* fo = (cnt && !p.fold.empty()) ? p.d_fold : nullptr;
   for (const auto& g : p.groups) {
     const int32_t ni = (int32_t)g.items.size();
     if (g.kind == 2)
@@ -378,9 +382,9 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode, int upd
     else if (g.kind == 3)
       launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, wp, ctx->stream);
     else
-      launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, upd_mode, upd_step, cnt, ctx->stream);
+      launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, upd_mode, upd_step, cnt, fo, ctx->stream);
   }
-  if (!p.fold.empty()) launch_fold_solo(s, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
+  if (!p.fold.empty() && !fo) launch_fold_solo(s, p.d_fold, (int32_t)p.fold.size(), p.max_p, ctx->stream);
   // gx branches: scratch group by scratch group (the groups reuse one scratch)
   for (const auto& g : p.gxg) {
     const int32_t* bl = p.d_gx + g.first;
@@ -936,13 +940,18 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     }
   }
   ctx->max_splits = max_splits;
-  // solo mode (build_plan): ~one tile per wave for a branch alone on the GPU
+  // solo mode (build_plan): few tiles per wave for a branch alone on the GPU -- one
+  // when its fold and update are separate launches, four when the gradient launch's
+  // last workgroup folds and updates (fewer slabs for that one workgroup to add)
+  int64_t solo_tpw = ctx->fuse_update_mode > 0 ? 4 : 1;
+  if (const char* e = getenv("BANN_SOLO_TPW")) solo_tpw = std::max(1, atoi(e));
   int64_t max_p_fused = 0;
   for (auto& h : ctx->br) {
     const BranchDev& d = h.dev;
     if (!d.fused) continue;
     max_p_fused = std::max<int64_t>(max_p_fused, h.P);
-    const int64_t per_item = d.fused == 1 ? 4 : 1;  // fx: 4 waves on their own tiles; fxl / wx: a tile at a time
+    // fx: 4 waves on their own tiles, solo_tpw tiles each; fxl / wx: a tile at a time
+    const int64_t per_item = d.fused == 1 ? 4 * solo_tpw : 1;
     h.solo_items = (int32_t)std::max<int64_t>(d.nsplits,
                                               std::min<int64_t>(2 * cus, (ntile + per_item - 1) / per_item));
   }
@@ -1472,6 +1481,7 @@ static std::string traj_graph_key(const bann_ctx* ctx, const Plan& p, int32_t L)
   put(p.n_small);
   put(p.n_large);
   put(p.max_p);
+  put(p.fuse_update);
   put((int64_t)p.fold.size());
   put((int64_t)(intptr_t)p.d_all);
   put((int64_t)(intptr_t)p.d_fold);
@@ -1497,14 +1507,25 @@ void clear_graphs(bann_ctx* ctx) {
 
 // the launches of one trajectory after traj_prepare: initial gradient (f(theta_0) -> pred0),
 // INIT update, L x (gradient, update), restore of the rejected branches' predictions
-static int traj_launches(bann_ctx* ctx, const Plan& p, int32_t L) {
-  int rc = run_grad(ctx, p, 2);
+// one leapfrog step's launches: gradient + update, or the gradient launch alone with
+// the update in its tail (a fuse_update plan)
+static int traj_step(bann_ctx* ctx, const Plan& p, int write_pred, int mode, int step) {
+  if (p.fuse_update) {
+    mark_predictions(ctx, p, false);
+    return run_grad(ctx, p, write_pred, mode, step);
+  }
+  const int rc = run_grad(ctx, p, write_pred);
   if (rc) return rc;
-  run_update(ctx, p, MODE_INIT, 0);
+  run_update(ctx, p, mode, step);
+  return BANN_OK;
+}
+
+static int traj_launches(bann_ctx* ctx, const Plan& p, int32_t L) {
+  int rc = traj_step(ctx, p, 2, MODE_INIT, 0);
+  if (rc) return rc;
   for (int k = 1; k <= L; ++k) {
-    rc = run_grad(ctx, p, k == L ? 1 : 0);
+    rc = traj_step(ctx, p, k == L ? 1 : 0, k < L ? MODE_STEP : MODE_LAST, k);
     if (rc) return rc;
-    run_update(ctx, p, k < L ? MODE_STEP : MODE_LAST, k);
   }
   launch_restore_pred(ctx->st, p.d_all, (int32_t)p.all.size(), ctx->stream);
   CK(hipGetLastError());
@@ -1570,8 +1591,13 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
   if (rc) return rc;
   rc = traj_prepare(ctx, p, std::max(L, 1), max_dh, step_mode, factor, eps, momentum, seed, u);
   if (rc) return rc;
-  if (L >= 1 && !ctx->rec_on && ctx->graph_replay) {  // the whole launch sequence as one graph launch
-    rc = traj_replay(ctx, p, L);
+  if (L >= 1 && !ctx->rec_on) {  // the whole launch sequence, as one graph launch or launch by launch
+    if (ctx->graph_replay) {
+      rc = traj_replay(ctx, p, L);
+    } else {
+      rc = traj_launches(ctx, p, L);
+      mark_predictions(ctx, p, true);
+    }
     if (rc) return rc;
     CK(hipStreamSynchronize(ctx->stream));
     return hmc_outputs(ctx, branches, nb, L, status_out, h_trace_out, uturn_out, log_density_out);

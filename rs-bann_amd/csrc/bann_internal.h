@@ -74,7 +74,7 @@ struct GradItem {
   int64_t part_at;  // float offset in DevState::part of the item's (first) slab
   int64_t rss_at;   // index in DevState::rss_part of its (first) rss partial
   int32_t tile0;    // forward-only fi pass: the group's tiles before this item (its index space)
-  int32_t pad_;
+  int32_t fold_ix;  // solo plans: index of the branch's FoldJob in the plan's fold list (else -1)
 };
 // solo-mode fold: a branch's ns slabs at part[part] / rss_part[rss] -> its slab 0
 struct FoldJob {
@@ -199,7 +199,8 @@ bool wx_exact();
 // upd_cnt != null: the fused leapfrog update (mode, step) in the tail -- the last workgroup of
 // each branch updates it (update_core.h); upd_cnt = one zeroed arrival counter per branch
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt, hipStream_t s);
+                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt,
+                          const FoldJob* folds, hipStream_t s);
 // forward-only fx pass (predictions into st.pred, no target / backward / partials)
 void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act, int full8,
                        hipStream_t s);

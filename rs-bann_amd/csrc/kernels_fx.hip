@@ -129,7 +129,7 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 template <int NL, int ACT, int NCH>
 __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred, int upd_mode, int upd_step,
-                    int32_t* __restrict__ upd_cnt) {
+                    int32_t* __restrict__ upd_cnt, const FoldJob* __restrict__ folds) {
   constexpr int NH = NL - 1;  // layers with activations
   constexpr int NW = FX_WAVES;
   constexpr int NS = 8 + (NH - 1) * 20;  // head statistics per wave
@@ -498,6 +498,16 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   }
   __syncthreads();
   float* part = st.part + it.part_at;
+  // a fused update with more than one workgroup per branch: the partials are handed
+  // to the branch's last arriving workgroup inside the launch, stored write-through
+  // (sc1: no release fence needed; MI355X_MICROARCH.md, inter-workgroup visibility)
+  const bool pub = upd_cnt != nullptr && (folds != nullptr || bd.nsplits > 1);
+  auto pst = [&](float* a, float v) {
+    if (pub)
+      __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      *a = v;
+  };
   float db0[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) db0[k] = (s_hs[0][k] + s_hs[1][k]) + (s_hs[2][k] + s_hs[3][k]);
@@ -514,7 +524,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       if (mk < m && c < bd.widths[0]) {
         const float mu = st.mu[bd.mk_off + mk], sg = st.sigma[bd.mk_off + mk];
         const float dbc = c == 0 ? db0[0] : c == 1 ? db0[1] : c == 2 ? db0[2] : db0[3];
-        part[bd.woff[0] + c * m + mk] = sg > 0.f ? (s - mu * dbc) / sg : 0.f;
+        pst(part + bd.woff[0] + c * m + mk, sg > 0.f ? (s - mu * dbc) / sg : 0.f);
       }
     }
   }
@@ -524,41 +534,56 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     for (int w = 0; w < NW; ++w) v += s_hs[w][lane];
     const int q = lane;
     if (q < 4) {
-      if (q < bd.widths[0]) part[bd.boff[0] + q] = v;
+      if (q < bd.widths[0]) pst(part + bd.boff[0] + q, v);
     } else if (q < 8) {
       const int j = q - 4;
-      if (j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+      if (j < bd.win[NL - 1]) pst(part + bd.woff[NL - 1] + j, v);
     } else {
       const int l = 1 + (q - 8) / 20, r = (q - 8) % 20;
       if (r < 4) {
-        if (r < bd.widths[l]) part[bd.boff[l] + r] = v;
+        if (r < bd.widths[l]) pst(part + bd.boff[l] + r, v);
       } else {
         const int j = (r - 4) >> 2, k = (r - 4) & 3;
-        if (j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = v;
+        if (j < bd.win[l] && k < bd.widths[l]) pst(part + bd.woff[l] + k * bd.win[l] + j, v);
       }
     }
   }
-  if (wave == 0 && lane == 0)
-    st.rss_part[it.rss_at] = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
+  if (wave == 0 && lane == 0) {
+    const double rs = (s_rss[0] + s_rss[1]) + (s_rss[2] + s_rss[3]);
+    if (pub)
+      __hip_atomic_store(st.rss_part + it.rss_at, rs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      st.rss_part[it.rss_at] = rs;
+  }
   if (upd_cnt) {
-    // fused leapfrog update (a one-round launch, bann_api.hip build_plan): the
-    // last of the branch's split workgroups to finish updates it here, with the
-    // update kernel's arithmetic and reduction order (update_small as 512 virtual
-    // threads), instead of a second launch.  Release the partials, count the
-    // arrival, acquire the other workgroups' partials.
-    // A branch of one split has one workgroup: this one, whose partial slab is
-    // visible to its own waves after a workgroup barrier (no counter, no fence).
+    // fused leapfrog update (bann_api.hip build_plan): the last of the branch's
+    // workgroups to finish updates it here, with the update kernel's arithmetic and
+    // reduction order (update_small as 512 virtual threads), instead of a second
+    // launch -- after folding the branch's slabs first in a solo plan (folds: the
+    // fold launch's order).  A branch of one split (no folds) has one workgroup:
+    // this one, whose slab its own waves see after a workgroup barrier.  Otherwise
+    // every wave drains its write-through partial stores, one lane counts the
+    // arrival (agent scope), and the last arriver acquires before reading the slabs.
     __shared__ int s_last;
     __shared__ double s_redd[4 * 8];
-    const bool single = bd.nsplits == 1;
-    if (!single) __threadfence();
+    if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) s_last = single || atomicAdd(&upd_cnt[b], 1) == bd.nsplits - 1;
+    const int narr = folds ? folds[it.fold_ix].nslab : bd.nsplits;
+    if (threadIdx.x == 0)
+      s_last = !pub || __hip_atomic_fetch_add(&upd_cnt[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == narr - 1;
     __syncthreads();
     if (s_last) {
-      if (!single) {
-        __threadfence();
-        if (threadIdx.x == 0) upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
+      if (pub) {
+        if (threadIdx.x == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
+        }
+        __syncthreads();
+      }
+      if (folds) {
+        fold_solo_all<64 * FX_WAVES>(st, folds[it.fold_ix], bd);
+        __syncthreads();  // slab 0 and its rss, written by this workgroup, read by update_small
       }
       float* s_th = reinterpret_cast<float*>(&s_x[0][0][0]);  // the tile slots are free: P <= 2048 floats
       update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
@@ -568,30 +593,33 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 
 template <int NL, int NCH>
 static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, int um, int us,
-                         int32_t* cnt, hipStream_t s) {
+                         int32_t* cnt, const FoldJob* fo, hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
   switch (act) {
-    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
-    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
-    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
-    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
-    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt); break;
+    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
   }
 }
 
 // full8: every branch of this launch group has exactly 8 chunks; upd_cnt != null:
-// the fused leapfrog update in the launch's tail (mode upd_mode, step upd_step)
+// the fused leapfrog update in the launch's tail (mode upd_mode, step upd_step),
+// folds != null: a solo plan's fold jobs, run by the tail before the update
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt, hipStream_t s) {
+                          int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt,
+                          const FoldJob* folds, hipStream_t s) {
   if (nitems <= 0) return;
   const int wp = write_pred, um = upd_mode, us = upd_step;
+  const FoldJob* fo = upd_cnt ? folds : nullptr;
   switch (L * 2 + (full8 ? 1 : 0)) {
-    case 4: launch_fx_nl<2, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
-    case 5: launch_fx_nl<2, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
-    case 6: launch_fx_nl<3, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
-    case 7: launch_fx_nl<3, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
-    case 8: launch_fx_nl<4, 0>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
-    case 9: launch_fx_nl<4, 8>(st, items, nitems, act, wp, um, us, upd_cnt, s); break;
+    case 4: launch_fx_nl<2, 0>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
+    case 5: launch_fx_nl<2, 8>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
+    case 6: launch_fx_nl<3, 0>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
+    case 7: launch_fx_nl<3, 8>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
+    case 8: launch_fx_nl<4, 0>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
+    case 9: launch_fx_nl<4, 8>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
     default: break;
   }
 }

@@ -300,22 +300,15 @@ void launch_fused_const(const DevState& st, const int32_t* branches, int32_t nb,
 // then lane 0 adds the 8 partials in q order -- a fixed order, one round of
 // memory latency instead of nslab / 16 (the single-branch step of the
 // sequential driver: 15 -> ~4 us)
-#define FOLD_Q 8
 __global__ void __launch_bounds__(256) k_fold_solo(DevState st, const FoldJob* __restrict__ jobs) {
   __shared__ float s_part[FOLD_Q][32];
   const FoldJob j = jobs[blockIdx.y];
   const BranchDev& bd = st.br[j.branch];
   const int P = bd.P;
   float* dst = st.part + bd.part_off;
-  const float* src = st.part + j.part;
   const int q = threadIdx.x >> 5, pl = threadIdx.x & 31;
   const int i = blockIdx.x * 32 + pl;
-  float v = 0.f;
-  if (i < P) {
-#pragma unroll 8
-    for (int s = q; s < j.nslab; s += FOLD_Q) v += src[(int64_t)s * P + i];
-  }
-  s_part[q][pl] = v;
+  s_part[q][pl] = i < P ? fold_solo_param(st.part + j.part, P, j.nslab, i, q) : 0.f;
   __syncthreads();
   if (q == 0 && i < P) {
     float t = s_part[0][pl];
@@ -324,14 +317,7 @@ __global__ void __launch_bounds__(256) k_fold_solo(DevState st, const FoldJob* _
     dst[i] = t;
     for (int s = 1; s < bd.nsplits; ++s) dst[(int64_t)s * P + i] = 0.f;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    double r = 0.0;
-#pragma unroll 16
-    for (int s = 0; s < j.nslab; ++s) r += st.rss_part[j.rss + s];
-    double* rd = st.rss_part + (int64_t)j.branch * st.max_splits;
-    rd[0] = r;
-    for (int s = 1; s < bd.nsplits; ++s) rd[s] = 0.0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) fold_solo_rss(st, j, bd);
 }
 
 void launch_fold_solo(const DevState& st, const FoldJob* jobs, int32_t njobs, int32_t max_p, hipStream_t s) {

@@ -7,6 +7,51 @@
 
 #include "bann_internal.h"
 
+// ---- solo-mode fold (build_plan): a branch's nslab partial slabs summed into its
+// slab 0, its other slabs and rss partials zeroed, so the update's fixed-order split
+// reduction sees the same sum.  Per parameter i: v_q = sum over slabs s = q, q + 8,
+// ... (increasing s) for q = 0..7, then v_0 + v_1 + ... + v_7 -- the order of
+// k_fold_solo's eight lanes per parameter, whoever computes it (kernels_update.hip
+// k_fold_solo: one block of 32 parameters per workgroup; the gradient launch's
+// fused tail: one thread per parameter, all eight v_q in registers) ----
+#define FOLD_Q 8
+__device__ __forceinline__ float fold_solo_param(const float* __restrict__ src, int P, int nslab, int i, int q) {
+  float v = 0.f;
+#pragma unroll 8
+  for (int s = q; s < nslab; s += FOLD_Q) v += src[(int64_t)s * P + i];
+  return v;
+}
+__device__ __forceinline__ void fold_solo_rss(const DevState& st, const FoldJob& j, const BranchDev& bd) {
+  double r = 0.0;
+#pragma unroll 16
+  for (int s = 0; s < j.nslab; ++s) r += st.rss_part[j.rss + s];
+  double* rd = st.rss_part + (int64_t)j.branch * st.max_splits;
+  rd[0] = r;
+  for (int s = 1; s < bd.nsplits; ++s) rd[s] = 0.0;
+}
+// the whole fold of job j by one workgroup of NT threads (thread t: parameters t, t + NT, ...)
+template <int NT>
+__device__ void fold_solo_all(const DevState& st, const FoldJob& j, const BranchDev& bd) {
+  const int P = bd.P;
+  float* dst = st.part + bd.part_off;
+  const float* src = st.part + j.part;
+  for (int i = threadIdx.x; i < P; i += NT) {
+    float v[FOLD_Q];
+#pragma unroll
+    for (int q = 0; q < FOLD_Q; ++q) v[q] = 0.f;
+    for (int s0 = 0; s0 < j.nslab; s0 += FOLD_Q)  // slab s0 + q -> v_q: each v_q in increasing s
+#pragma unroll
+      for (int q = 0; q < FOLD_Q; ++q)
+        if (s0 + q < j.nslab) v[q] += src[(int64_t)(s0 + q) * P + i];
+    float t = v[0];
+#pragma unroll
+    for (int q = 1; q < FOLD_Q; ++q) t += v[q];
+    dst[i] = t;
+    for (int s = 1; s < bd.nsplits; ++s) dst[(int64_t)s * P + i] = 0.f;
+  }
+  if (threadIdx.x == 0) fold_solo_rss(st, j, bd);
+}
+
 // NV doubles summed over the workgroup in one pass (one barrier pair)
 template <int NT, int NV>
 __device__ void block_sum_n(double (&v)[NV], double* red) {

@@ -1085,3 +1085,44 @@ def test_fused_update_session_bitwise(Ctx, monkeypatch, shape, fused):
             assert np.array_equal(p0[b], p1[b]), b
         assert np.array_equal(d0, d1)
     assert sum(a for _, a, _, _ in outs[1]) > 0   # some trajectory accepted: the fused tail moved the chain
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_solo_hmc_step_bitwise(Ctx, monkeypatch, graph):
+    """the sequential driver's single-branch trajectories (solo plans: the branch
+    re-split over many workgroups): with the fold and the update in the gradient
+    launch's tail (the default; the last arriving workgroup adds the branch's
+    slabs in k_fold_solo's order, then updates it) every trajectory -- status, -H
+    trace, parameters, prediction rows -- has the bits of the separate fold and
+    update launches (BANN_FUSE_UPDATE=0), launched one by one or replayed as a graph."""
+    rng = np.random.default_rng(83)
+    n, nb, m = 20000, 3, 500
+    g = O.synthetic_genotypes(rng, n, nb * m)
+    specs = [dict(snps=np.arange(b * m, (b + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, [4, 4, 1])),
+                  y=rng.normal(size=n).astype(np.float32)) for b in range(nb)]
+    monkeypatch.setenv("BANN_SOLO_TPW", "4")   # the same solo split in both contexts
+    outs = []
+    for fuse in ("0", None):
+        if fuse is None:
+            monkeypatch.delenv("BANN_FUSE_UPDATE", raising=False)
+        else:
+            monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
+        ctx = build_context(Ctx, g, specs)
+        ctx.set_graph_replay(graph)
+        res = []
+        for it, (b, L, f) in enumerate([(0, 5, 0.3), (1, 3, 1.0), (2, 6, 0.2), (0, 4, 0.5), (1, 5, 0.05)]):
+            r = ctx.hmc_step([b], L, 10.0, step_factor=f, seed=500 + it)
+            res.append((r["status"].copy(), r["trace"].copy(), [ctx.get_params(k) for k in range(nb)],
+                        [ctx.predict(k) for k in range(nb)]))
+        outs.append(res)
+        ctx.close()
+    acc = 0
+    for (s0, t0, p0, f0), (s1, t1, p1, f1) in zip(*outs):
+        assert np.array_equal(s0, s1)
+        assert np.array_equal(t0, t1, equal_nan=True)
+        for k in range(nb):
+            assert np.array_equal(p0[k], p1[k]), k
+            assert np.array_equal(f0[k], f1[k]), k
+        acc += int(s1[0] == 0)
+    assert acc > 0
