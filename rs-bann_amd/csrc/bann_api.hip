@@ -270,7 +270,10 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       single = single && h.dev.nsplits == 1;
     }
     // solo plans: the last arriving workgroup folds the branch's slabs, then updates it
-    p.fuse_update = ok && items > 0 && (solo || single || (ctx->fuse_update_mode > 1 && items <= 2ll * ctx->cus));
+    // (one-split plans, C3: measured +0.3 % per launch in round 3 -- the update's dependent round trips
+    // lengthen every workgroup's tail -- so only with BANN_FUSE_UPDATE=1)
+    p.fuse_update = ok && items > 0 &&
+                    (solo || (ctx->fuse_update_mode > 1 && (single || items <= 2ll * ctx->cus)));
   }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
   std::stable_sort(p.gx.begin(), p.gx.end(),

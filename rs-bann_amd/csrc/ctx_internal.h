@@ -88,10 +88,10 @@ struct bann_ctx {
   int64_t xi_bytes = 0;
   int32_t cus = 256;
   int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
-  // the update in the gradient launch's tail: 1 (default) = plans whose branches have one
-  // split each (the workgroup that computed a branch's gradient updates it: no counter, no
-  // fence); 2 (BANN_FUSE_UPDATE=1) = also one-round multi-split plans (last arriver, agent
-  // fences: at the N = 8 shard 0.292 vs 0.204 ms per step, so not by default); 0 = never
+  // the update in the gradient launch's tail: 1 (default) = solo plans (the sequential
+  // driver: the last arriving workgroup folds and updates; one launch per leapfrog step
+  // instead of three); 2 (BANN_FUSE_UPDATE=1) = also one-split plans (the branch's one
+  // workgroup, no counter or fence) and one-round multi-split plans (last arriver); 0 = never
   int fuse_update_mode = 1;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;

@@ -1046,7 +1046,7 @@ def test_forward_fi_matches_lds_forward(Ctx, n, monkeypatch):
     assert np.array_equal(preds[0], preds[1])
 
 
-@pytest.mark.parametrize("shape,fused", [("multi", "1"), ("single", None)])
+@pytest.mark.parametrize("shape,fused", [("multi", "1"), ("single", "1")])
 def test_fused_update_session_bitwise(Ctx, monkeypatch, shape, fused):
     """the leapfrog update in the gradient launch's tail (update_small as 512
     virtual threads) gives the bits of the separate update launches
@@ -1054,8 +1054,8 @@ def test_fused_update_session_bitwise(Ctx, monkeypatch, shape, fused):
       multi: a one-round multi-split fx plan (the N = 8 shard's shape: here 70
         branches x 7 splits), the last arriving workgroup of each branch updates
         it (BANN_FUSE_UPDATE=1);
-      single: one split per branch (C3's shape: 600 branches on 2 048
-        individuals), each branch's one workgroup updates it (the default)."""
+      single: one split per branch (C3's shape: 600 branches on 1 024
+        individuals), each branch's one workgroup updates it (BANN_FUSE_UPDATE=1)."""
     rng = np.random.default_rng(77)
     n, nb, m = (2048, 70, 60) if shape == "multi" else (1024, 600, 20)
     g = O.synthetic_genotypes(rng, n, nb * m)

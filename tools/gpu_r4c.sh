@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -1 $OUT/tests.log
 TAG=$T/net VARIANTS="- BANN_FWD_FI=0" BARGS="--sampler network --steps 20 --warmup 2" bash tools/gpu_c3ab.sh || exit 1
 TAG=$T/seq VARIANTS="- BANN_FUSE_UPDATE=0,BANN_SOLO_TPW=1" BARGS="--sampler sequential --steps 20 --warmup 0" bash tools/gpu_c3ab.sh || exit 1
-TAG=$T/c3 VARIANTS="- BANN_FUSE_UPDATE=0" bash tools/gpu_c3ab.sh || exit 1
+TAG=$T/c3 VARIANTS="- BANN_FUSE_UPDATE=1" bash tools/gpu_c3ab.sh || exit 1
 TAG=$T/shard VARIANTS="- BANN_FUSE_UPDATE=1" BARGS="--emulate-shard 8 --steps 20 --warmup 5" bash tools/gpu_c3ab.sh || exit 1
 TAG=$T/c2 VARIANTS="- BANN_FXL_CPW=8" BARGS="--config c2 --steps 20 --warmup 5" bash tools/gpu_c3ab.sh || exit 1
 for f in ${C5F:-0.002 0.005}; do
