@@ -12,6 +12,7 @@
 // net.rs:292-300 over ranks) and (b) one HMC state over all branches of all
 // ranks (network mode).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -222,6 +223,8 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   // fx-only plans: the gradient kernel reads e itself (DevState::nete), no per-branch targets
   bool fx_only = p.gx.empty();
   for (const auto& g : p.groups) fx_only = fx_only && g.kind == 1;
+  if (const char* e = getenv("BANN_NET_ERR"))  // 0: per-branch targets for every kind (diagnostics)
+    fx_only = fx_only && atoi(e) != 0;
   ctx->st.nete = fx_only ? ctx->d_netsum : nullptr;
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
   // (launch timing, when enabled: forward, all-reduce, gradient and update spans)

@@ -244,3 +244,44 @@ def test_library_rccl_beside_torch_rccl():
     mp.spawn(_torch_rccl_worker, args=(_free_port(), out), nprocs=1, join=True)
     assert out["info"]["kind"] == "rccl" and out["info"]["backend_ranks"] == 1
     assert out["same"] and out["torch_sum"] == 1.0
+
+
+@pytest.mark.parametrize("net_err", ["1", "0"])
+def test_network_hmc_fx_only_matches_oracle(monkeypatch, net_err):
+    """a network of fx branches only (C3's kind): the gradient kernel reads the
+    network's output error e = sum f + bias - y itself (DevState::nete,
+    BANN_NET_ERR=1, the default) instead of per-branch targets y_b = f_b - e; both
+    reproduce the oracle's -H trace, status and parameters"""
+    monkeypatch.setenv("BANN_NET_ERR", net_err)
+    rng = np.random.default_rng(31)
+    n = 1500
+    shapes = [(60, [4, 4, 1]), (100, [4, 4, 1]), (33, [4, 3, 1]), (64, [4, 4, 1])]
+    M = sum(m for m, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior="ridge_ard"))))
+        off += m
+    ctx = _context(g, specs, range(len(specs)))
+    assert all(ctx.kernel_path(b) == "fused" for b in range(len(specs)))
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    f = sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+    y = (f + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    L = 8
+    for u in (0.3, 0.9):
+        eps, mom = _draws(rng, specs, L)
+        res = ctx.network_hmc_step(y, L, bias=0.1, lambda_e=2.0, eps=np.concatenate(eps),
+                                   momentum=np.concatenate(mom), u=u)
+        brs = [s["branch"].copy() for s in specs]
+        out = O.network_hmc_step(brs, Xs, y, 0.1, 2.0, [e.astype(np.float64) for e in eps],
+                                 [p.astype(np.float64) for p in mom], L, 10.0, u)
+        assert res["status"] == out["status"], (res["status"], out["status"], res["trace"], out["trace"])
+        tr = np.asarray(out["trace"])
+        assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (res["trace"], tr)
+        for b, br in enumerate(brs):
+            assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+        for s, br in zip(specs, brs):
+            s["branch"] = f32_branch(br)
+    ctx.close()

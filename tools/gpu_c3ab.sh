@@ -3,7 +3,7 @@
 # ("-" = defaults), BARGS = the bench arguments (default: the C3 line)
 set -o pipefail
 R=$(pwd); OUT=$R/gpurun_out/${TAG:-c3ab}; mkdir -p $OUT
-j() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; print('$1', round(d['value'],2), 'ms', round(d['ms_per_step'],4), 'k', round(r['kernel_ms'],4), 'upd', round(r['update_kernel_ms'],4), 'acc', d['accept_rate'])"; }
+j() { python -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; print('$1', round(d['value'],2), 'ms', round(d['ms_per_step'],4), 'k', round(r['kernel_ms'],4), 'upd', round(r['update_kernel_ms'],4), 'acc', d['accept_rate'], (d.get('accept_rate_trajectories') or {}).get('rate'))"; }
 i=0
 for rep in 1 2; do
   for v in ${VARIANTS:--}; do
