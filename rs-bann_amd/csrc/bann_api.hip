@@ -270,10 +270,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       single = single && h.dev.nsplits == 1;
     }
     // solo plans: the last arriving workgroup folds the branch's slabs, then updates it
-    // (one-split plans, C3: measured +0.3 % per launch in round 3 -- the update's dependent round trips
-    // lengthen every workgroup's tail -- so only with BANN_FUSE_UPDATE=1)
-    p.fuse_update = ok && items > 0 &&
-                    (solo || (ctx->fuse_update_mode > 1 && (single || items <= 2ll * ctx->cus)));
+    p.fuse_update = ok && items > 0 && (solo || single || items <= 2ll * ctx->cus);
   }
   // gx branches: grouped by scratch group, one tile prefix array per GEMM phase
   std::stable_sort(p.gx.begin(), p.gx.end(),
@@ -473,7 +470,7 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   bann_ctx* ctx = new bann_ctx();
   ctx->device = device;
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
-  if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 2 : 0;
+  if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return BANN_E_HIP;
@@ -943,10 +940,9 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     }
   }
   ctx->max_splits = max_splits;
-  // solo mode (build_plan): few tiles per wave for a branch alone on the GPU -- one
-  // when its fold and update are separate launches, four when the gradient launch's
-  // last workgroup folds and updates (fewer slabs for that one workgroup to add)
-  int64_t solo_tpw = ctx->fuse_update_mode > 0 ? 4 : 1;
+  // solo mode (build_plan): ~one tile per wave for a branch alone on the GPU
+  // (BANN_SOLO_TPW: more tiles per wave, fewer slabs to fold)
+  int64_t solo_tpw = 1;
   if (const char* e = getenv("BANN_SOLO_TPW")) solo_tpw = std::max(1, atoi(e));
   int64_t max_p_fused = 0;
   for (auto& h : ctx->br) {

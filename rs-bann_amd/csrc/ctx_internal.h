@@ -88,11 +88,12 @@ struct bann_ctx {
   int64_t xi_bytes = 0;
   int32_t cus = 256;
   int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
-  // the update in the gradient launch's tail: 1 (default) = solo plans (the sequential
-  // driver: the last arriving workgroup folds and updates; one launch per leapfrog step
-  // instead of three); 2 (BANN_FUSE_UPDATE=1) = also one-split plans (the branch's one
-  // workgroup, no counter or fence) and one-round multi-split plans (last arriver); 0 = never
-  int fuse_update_mode = 1;
+  // the update in the gradient launch's tail (BANN_FUSE_UPDATE=1; same bits either way):
+  // one-split plans (the branch's one workgroup), one-round multi-split plans and solo
+  // plans (the last arriving workgroup; solo: it folds the branch's slabs first).  Off
+  // by default: measured slower everywhere (r4c: C3 747.7 vs 752.9 steps/s, N = 8 shard
+  // 4 269 vs 4 531, sequential driver 6.5 vs 21.9 -- one workgroup adding 49 slabs)
+  int fuse_update_mode = 0;
   uint8_t* d_dig = nullptr;
   FusedConst* d_fc = nullptr;
   float *d_mub = nullptr, *d_sigb = nullptr;

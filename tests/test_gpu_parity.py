@@ -1091,10 +1091,10 @@ def test_fused_update_session_bitwise(Ctx, monkeypatch, shape, fused):
 def test_fused_solo_hmc_step_bitwise(Ctx, monkeypatch, graph):
     """the sequential driver's single-branch trajectories (solo plans: the branch
     re-split over many workgroups): with the fold and the update in the gradient
-    launch's tail (the default; the last arriving workgroup adds the branch's
+    launch's tail (BANN_FUSE_UPDATE=1: the last arriving workgroup adds the branch's
     slabs in k_fold_solo's order, then updates it) every trajectory -- status, -H
     trace, parameters, prediction rows -- has the bits of the separate fold and
-    update launches (BANN_FUSE_UPDATE=0), launched one by one or replayed as a graph."""
+    update launches (the default), launched one by one or replayed as a graph."""
     rng = np.random.default_rng(83)
     n, nb, m = 20000, 3, 500
     g = O.synthetic_genotypes(rng, n, nb * m)
@@ -1103,11 +1103,8 @@ def test_fused_solo_hmc_step_bitwise(Ctx, monkeypatch, graph):
                   y=rng.normal(size=n).astype(np.float32)) for b in range(nb)]
     monkeypatch.setenv("BANN_SOLO_TPW", "4")   # the same solo split in both contexts
     outs = []
-    for fuse in ("0", None):
-        if fuse is None:
-            monkeypatch.delenv("BANN_FUSE_UPDATE", raising=False)
-        else:
-            monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("BANN_FUSE_UPDATE", fuse)
         ctx = build_context(Ctx, g, specs)
         ctx.set_graph_replay(graph)
         res = []

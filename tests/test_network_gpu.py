@@ -246,16 +246,17 @@ def test_library_rccl_beside_torch_rccl():
     assert out["same"] and out["torch_sum"] == 1.0
 
 
-@pytest.mark.parametrize("net_err", ["1", "0"])
-def test_network_hmc_fx_only_matches_oracle(monkeypatch, net_err):
+@pytest.mark.parametrize("net_err,big", [("1", False), ("0", False), ("1", True), ("0", True)])
+def test_network_hmc_fx_only_matches_oracle(monkeypatch, net_err, big):
     """a network of fx branches only (C3's kind): the gradient kernel reads the
     network's output error e = sum f + bias - y itself (DevState::nete,
     BANN_NET_ERR=1, the default) instead of per-branch targets y_b = f_b - e; both
     reproduce the oracle's -H trace, status and parameters"""
     monkeypatch.setenv("BANN_NET_ERR", net_err)
     rng = np.random.default_rng(31)
-    n = 1500
-    shapes = [(60, [4, 4, 1]), (100, [4, 4, 1]), (33, [4, 3, 1]), (64, [4, 4, 1])]
+    # big: C3's branch shape (8 full marker chunks: the full8 kernel) and many tiles per wave
+    n = 20000 if big else 1500
+    shapes = ([(500, [4, 4, 1])] * 4) if big else [(60, [4, 4, 1]), (100, [4, 4, 1]), (33, [4, 3, 1]), (64, [4, 4, 1])]
     M = sum(m for m, _ in shapes)
     g = O.synthetic_genotypes(rng, n, M)
     specs, off = [], 0
