@@ -80,6 +80,10 @@ TUNED_FACTORS = {
     ("c5", "branch", False): (0.1, 20),
     ("c5", "branch", True): (0.02, 20),       # bf16-rounded hidden activations: energy error
     ("c3def", "branch", False): (0.02, 10),
+    # C5's joint state (4 000 branches, 21 M parameters): 0.01 and 0.005 diverge, 0.001
+    # rejects, 0.0005 accepts (2 of 2 trajectories at L = 20, r4c / r4d)
+    ("c5", "network", False): (0.0005, 20),
+    ("c5", "network", True): (0.0005, 20),
 }
 
 
@@ -395,6 +399,11 @@ def main():
             # the Metropolis uniform: drawn by the library on rank 0 (seed) and shared
             r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov",
                                      step_factor=args.step_factor, seed=seed)
+            if os.environ.get("BANN_BENCH_TRACE"):   # diagnostics: the network -H trace on stderr
+                th = np.concatenate([ctx.get_params(b) for b in range(nb)]).astype(np.float64)
+                log(json.dumps({"seed": seed, "status": int(r["status"]), "theta_ss": float(th @ th),
+                                "pred_ss": float(np.sum(ctx.predict_many(list(range(min(nb, 50)))).astype(np.float64) ** 2)),
+                                "trace": [float(v) for v in r["trace"][:4]]}))
             return float(r["status"] == 0) * nb
         ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
         ctx.leapfrog_steps(L)
@@ -435,9 +444,16 @@ def main():
     # power controller settles: profiles/r03a_transient.md)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
+    # the back-to-back session is a (2-step) branch-sampler trajectory: it would move
+    # every branch against its own target -- a Jacobi step of the whole network, which
+    # the network and sequential samplers must not see -- so the chain is put back after it
+    snap = [ctx.get_params(b) for b in branches]
     ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99 + rank)
     b2b_grad_ms, b2b_upd_ms = ctx.profile_session(args.profile_iters)
     ctx.leapfrog_end()
+    for b in branches:
+        ctx.set_params(b, snap[b])
+    del snap
     timing = args.sampler == "branch" and not args.no_launch_timing
     if timing:   # HIP events around every gradient / update launch of the timed trajectory
         ctx.launch_timing(reset=True)
