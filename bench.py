@@ -400,10 +400,7 @@ def main():
             r = ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov",
                                      step_factor=args.step_factor, seed=seed)
             if os.environ.get("BANN_BENCH_TRACE"):   # diagnostics: the network -H trace on stderr
-                th = np.concatenate([ctx.get_params(b) for b in range(nb)]).astype(np.float64)
-                log(json.dumps({"seed": seed, "status": int(r["status"]), "theta_ss": float(th @ th),
-                                "pred_ss": float(np.sum(ctx.predict_many(list(range(min(nb, 50)))).astype(np.float64) ** 2)),
-                                "trace": [float(v) for v in r["trace"][:4]]}))
+                log(json.dumps({"seed": seed, "status": int(r["status"]), "trace": [float(v) for v in r["trace"]]}))
             return float(r["status"] == 0) * nb
         ctx.leapfrog_begin(branches, L, 10.0, "izmailov", args.step_factor, seed=seed)
         ctx.leapfrog_steps(L)
@@ -441,20 +438,29 @@ def main():
     # times without changing the chain) -- untimed work that also lets the GPU's
     # clock settle under the HBM load before the timed trajectory (the first
     # ~10 gradient launches after a light phase run up to 30 % slow while the
-    # power controller settles: profiles/r03a_transient.md)
+    # power controller settles: profiles/r03a_transient.md).
+    # The session is a branch-sampler trajectory (every branch against its own
+    # target: a Jacobi step of the whole network), which the network and
+    # sequential samplers must not see: the network sampler times its own
+    # gradient launches instead and runs no session; the sequential driver runs it
+    # first and puts the parameters back (the warmup sweep then re-settles the clock).
+    def b2b_session(restore):
+        snap = [ctx.get_params(b) for b in branches] if restore else None
+        ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99 + rank)
+        r = ctx.profile_session(args.profile_iters)
+        ctx.leapfrog_end()
+        if restore:
+            for b in branches:
+                ctx.set_params(b, snap[b])
+        return r
+    b2b_grad_ms = b2b_upd_ms = None
+    if args.sampler == "sequential" or (args.sampler == "network" and args.no_launch_timing):
+        b2b_grad_ms, b2b_upd_ms = b2b_session(restore=True)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
-    # the back-to-back session is a (2-step) branch-sampler trajectory: it would move
-    # every branch against its own target -- a Jacobi step of the whole network, which
-    # the network and sequential samplers must not see -- so the chain is put back after it
-    snap = [ctx.get_params(b) for b in branches]
-    ctx.leapfrog_begin(branches, 2, 10.0, "izmailov", args.step_factor, seed=99 + rank)
-    b2b_grad_ms, b2b_upd_ms = ctx.profile_session(args.profile_iters)
-    ctx.leapfrog_end()
-    for b in branches:
-        ctx.set_params(b, snap[b])
-    del snap
-    timing = args.sampler == "branch" and not args.no_launch_timing
+    if args.sampler == "branch":
+        b2b_grad_ms, b2b_upd_ms = b2b_session(restore=False)
+    timing = args.sampler in ("branch", "network") and not args.no_launch_timing
     if timing:   # HIP events around every gradient / update launch of the timed trajectory
         ctx.launch_timing(reset=True)
         ctx.set_launch_timing(True)
@@ -472,6 +478,8 @@ def main():
     if timing:
         ctx.set_launch_timing(False)
         grad_ms, upd_ms, n_launch = ctx.launch_timing(reset=True)
+        if args.sampler == "network":
+            ctx.network_timing(reset=True)
     else:
         grad_ms, upd_ms, n_launch = b2b_grad_ms, b2b_upd_ms, 0
     if dist is not None:
