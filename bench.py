@@ -521,7 +521,10 @@ def main():
     # fused kernel streams the 2-bit codes, so counting int8 bytes would
     # overstate the achieved bandwidth 4x.)
     x_bytes = ((n + 3) // 4) * m_b * nb
-    y_bytes = 4 * n * nb
+    # network sampler on the fx path: every branch reads the one network error vector
+    # (DevState::nete), L2-resident, instead of a target row of its own
+    net_err = args.sampler == "network" and path == "fused" and os.environ.get("BANN_NET_ERR", "1") != "0"
+    y_bytes = 4 * n * (1 if net_err else nb)
     alg_bytes = x_bytes + y_bytes
     achieved = alg_bytes / (grad_ms * 1e-3) / 1e9
     # wide branches: the dominant work is the hidden-layer GEMMs on MFMA --
@@ -602,12 +605,15 @@ def main():
                                               "trajectory" if n_launch else "back-to-back launches (bann_profile_session)"),
                          "kernel_ms_back_to_back": b2b_grad_ms, "alg_bytes_per_launch": alg_bytes,
                          "packed_bytes_per_launch": ctx.packed_genotype_bytes,
-                         "alg_bytes_basis": "2-bit genotypes (n*m_b/4) + 4n target bytes per branch", "update_kernel_ms": upd_ms},
+                         "alg_bytes_basis": ("2-bit genotypes (n*m_b/4) per branch + the 4n-byte network error once"
+                                             if net_err else "2-bit genotypes (n*m_b/4) + 4n target bytes per branch"),
+                         "update_kernel_ms": upd_ms},
             "cpu_baseline": cpu,
             "accept_rate": acc_all / nb_all,
             **({"accept_rate_trajectories": {"trajectories": len(accs), "rate": float(np.mean(accs))}}
                if n_extra else {}),
             "step_factor": args.step_factor,
+            "sampler": args.sampler,
             "setup_s": setup_s,
         }
         if netcheck is not None:

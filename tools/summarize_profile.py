@@ -27,7 +27,10 @@ bench = json.loads(open(os.path.join(out, "bench_trace.json")).read().strip().sp
 # one k_step_sizes launch (traj_prepare)
 trace.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(trace) if "k_step_sizes" in r["Kernel_Name"]]
-t_ix = 2 + (1 if bench.get("network_check") else 0) - (0 if bench.get("warmup") else 1)
+sampler = bench.get("sampler") or ("network" if "network-joint" in bench["config"]["workload"] else "branch")
+# trajectories before the timed one: the network check, the warmup, and (branch sampler) the
+# back-to-back session
+t_ix = (1 if bench.get("network_check") else 0) + (1 if bench.get("warmup") else 0) + (1 if sampler == "branch" else 0)
 timed = trace[starts[t_ix]:starts[t_ix + 1] if len(starts) > t_ix + 1 else len(trace)] if len(starts) > t_ix else []
 tgrad = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_fused_grad" in r["Kernel_Name"]]
 tupd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_update" in r["Kernel_Name"]]
@@ -128,7 +131,7 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
         f.write("\n")
     f.write(f"bench.py's own HIP-event timing of the gradient launch: {bench['roofline']['kernel_ms']:.4f} ms "
             f"({bench['roofline'].get('kernel_ms_source', '')}); back-to-back "
-            f"{bench['roofline'].get('kernel_ms_back_to_back', float('nan')):.4f} ms\n\n")
+            f"{bench['roofline'].get('kernel_ms_back_to_back') or float('nan'):.4f} ms\n\n")
     f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB "
             f"({write_pred/1e9:.4f} GB at a trajectory's first/last launch, predictions included); "
             f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
