@@ -139,12 +139,77 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
       mus[r][c] = j < m ? st.mu[bd.mk_off + j] : 0.f;
       sgs[r][c] = j < m ? st.sigma[bd.mk_off + j] : 0.f;
     }
+  // Every global load of the step is issued in batches, the sums keep their order:
+  // the split partials two slabs at a time for all of the thread's parameters (a
+  // one-at-a-time loop waited once per slab and parameter: 4 x 4 round trips at the
+  // N = 8 shard's four splits), the parameter arrays for all parameters at once.
+  const int ns = bd.nsplits;
+  const double* rsp = st.rss_part + (int64_t)b * st.max_splits;
   double rss = 0.0;
-  for (int s = 0; s < bd.nsplits; ++s) rss += st.rss_part[(int64_t)b * st.max_splits + s];
+  {
+    int s = 0;
+    for (; s + 1 < ns; s += 2) {
+      const double r0 = rsp[s], r1 = rsp[s + 1];
+      rss += r0;
+      rss += r1;
+    }
+    if (s < ns) rss += rsp[s];
+  }
   const float le = st.netmode ? st.net_le : st.eprec[b];  // network mode: the network error precision
   const bool lasso = (bd.prior == 2 || bd.prior == 3);
   constexpr int CAP = upd_cap<NV_T>();
   float th[R][CAP], gr[R][CAP], pm[R][CAP], ep[R][CAP], t0[R][CAP];
+  float dd[R][CAP];  // d(rss/2)/dtheta: the split slabs summed in order
+  const bool need_t0 = mode == MODE_STEP || mode == MODE_LAST;
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < CAP; ++c) dd[r][c] = 0.f;
+  {
+    const float* pp = st.part + bd.part_off;
+    int s = 0;
+    for (; s + 1 < ns; s += 2) {
+      float v0[R][CAP], v1[R][CAP];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < CAP; ++c) {
+          const int i = threadIdx.x + r * NT + c * NV_T;
+          v0[r][c] = i < P ? pp[(int64_t)s * P + i] : 0.f;
+          v1[r][c] = i < P ? pp[(int64_t)(s + 1) * P + i] : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < CAP; ++c) {
+          dd[r][c] += v0[r][c];
+          dd[r][c] += v1[r][c];
+        }
+    }
+    if (s < ns)
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < CAP; ++c) {
+          const int i = threadIdx.x + r * NT + c * NV_T;
+          dd[r][c] += i < P ? pp[(int64_t)s * P + i] : 0.f;
+        }
+  }
+  float lmv[R][CAP], llv[R][CAP];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < CAP; ++c) {
+      const int i = threadIdx.x + r * NT + c * NV_T;
+      const bool in = i < P;
+      th[r][c] = in ? st.theta[base + i] : 0.f;
+      lmv[r][c] = in ? st.lam[base + i] : 0.f;
+      llv[r][c] = in ? st.lamld[base + i] : 0.f;
+      pm[r][c] = in ? st.mom[base + i] : 0.f;
+      ep[r][c] = in ? st.eps[base + i] : 0.f;
+      t0[r][c] = (in && need_t0) ? st.theta0[base + i] : 0.f;
+      gr[r][c] = 0.f;
+    }
   double sums[R][3];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -153,16 +218,10 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
 #pragma unroll
     for (int c = 0; c < CAP; ++c) {
       const int i = t + c * NV_T;
-      th[r][c] = gr[r][c] = pm[r][c] = ep[r][c] = t0[r][c] = 0.f;
       if (i >= P) continue;
-      float d = 0.f;
-      for (int s = 0; s < bd.nsplits; ++s) d += st.part[bd.part_off + (int64_t)s * P + i];
-      th[r][c] = st.theta[base + i];
-      const float lm = st.lam[base + i];
-      const float ll = st.lamld[base + i];
-      pm[r][c] = st.mom[base + i];
-      ep[r][c] = st.eps[base + i];
-      if (mode == MODE_STEP || mode == MODE_LAST) t0[r][c] = st.theta0[base + i];
+      const float d = dd[r][c];
+      const float lm = lmv[r][c];
+      const float ll = llv[r][c];
       const float sgn = th[r][c] > 0.f ? 1.f : (th[r][c] < 0.f ? -1.f : 0.f);  // af_helpers.rs:53-58
       const float reg = lasso ? lm * sgn : lm * th[r][c];
       gr[r][c] = -(le * d + reg);  // log_density_gradient (branch_sampler.rs:380-391)
