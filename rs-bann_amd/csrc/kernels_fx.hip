@@ -212,7 +212,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   // LDS-DMA of the NEXT tile is spread over the current tile's forward phase
   // (one 1 KiB piece per chunk, the target piece in the head): issued in one
   // burst the pieces back-pressure the wave for thousands of cycles.
+  // the last chunk's padding rows (markers >= m) are not streamed (C3: 12 of 512 rows):
+  // their W0 digits are zero, so whatever the slot holds there adds nothing to Z0, and
+  // their dW0 rows are dropped.  Lane L moves record L of a chunk: window L >> 4 at
+  // position L & 15 holds row 16 (L >> 4) + ((L & 15) - 8 ((L >> 4) & 1)) & 15.
+  // (Row 0 is never padding, so the wave's instruction -- one vmcnt count -- always issues.)
+  const bool pad_row = 64 * (nch - 1) + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
   auto issue_chunk = [&](int tt, int sl, int c) {
+    if (c == nch - 1 && pad_row) return;
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
   auto issue_y = [&](int tt, int sl) {
@@ -712,7 +719,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
   float* predb = st.pred + bd.y_off;
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
+  // the last chunk's padding rows are not streamed (as in k_fused_grad_fx)
+  const bool pad_row = 64 * (nch - 1) + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
   auto issue_chunk = [&](int tt, int sl, int c) {
+    if (c == nch - 1 && pad_row) return;
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
 
