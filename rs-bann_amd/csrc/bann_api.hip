@@ -1843,6 +1843,17 @@ void tm_mark(bann_ctx* ctx, int32_t kind) {
 }
 
 // after the stream has drained: elapsed time of every (start, end) pair of marks
+// a mark that starts where the previous mark (an update's end) left off, with nothing
+// enqueued in between: the same event, no second record on the stream
+void tm_mark_follow(bann_ctx* ctx, int32_t kind) {
+  if (!ctx->tm_on) return;
+  if (!ctx->tm_marks.empty() && ctx->tm_marks.back().second == TM_UPD1) {
+    ctx->tm_marks.push_back({ctx->tm_marks.back().first, kind});
+    return;
+  }
+  tm_mark(ctx, kind);
+}
+
 int tm_resolve(bann_ctx* ctx) {
   for (size_t i = 0; i + 1 < ctx->tm_marks.size(); ++i) {
     const auto a = ctx->tm_marks[i], b = ctx->tm_marks[i + 1];
@@ -1945,7 +1956,7 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   if (k < 0 || ctx->lf_step + k > ctx->lf_L) return fail(ctx, BANN_E_ARG, "steps beyond the trajectory length");
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
-    tm_mark(ctx, TM_GRAD0);
+    tm_mark_follow(ctx, TM_GRAD0);  // the previous step's (or the session start's) end
     int rc = grad_update(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
     if (rc) return rc;
     tm_mark(ctx, TM_UPD1);

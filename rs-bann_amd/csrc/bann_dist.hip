@@ -229,7 +229,7 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
   // (launch timing, when enabled: forward, all-reduce, gradient and update spans)
   auto forward_and_targets = [&](int k) -> int {
-    tm_mark(ctx, TM_FWD0);
+    tm_mark_follow(ctx, TM_FWD0);  // the previous step's update end
     int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
     if (r) return r;
     tm_mark(ctx, TM_FWD1);

@@ -219,4 +219,5 @@ int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t 
 // in-trajectory launch timing (bann_set_launch_timing): event marks on the context stream
 enum { TM_GRAD0 = 0, TM_GRAD1 = 1, TM_UPD1 = 2, TM_AR0 = 3, TM_AR1 = 4, TM_FWD0 = 5, TM_FWD1 = 6 };
 void tm_mark(bann_ctx* ctx, int32_t kind);
+void tm_mark_follow(bann_ctx* ctx, int32_t kind);
 int tm_resolve(bann_ctx* ctx);  // after the stream has drained
