@@ -1829,7 +1829,8 @@ extern "C" int bann_branch_get_trajectory_joint(bann_ctx* ctx, int32_t b, int32_
 // mode adds TM_FWD0/1 around the forward launch and TM_AR0/1 around the all-reduce
 void tm_mark(bann_ctx* ctx, int32_t kind) {
   if (!ctx->tm_on) return;
-  const size_t k = ctx->tm_marks.size();
+  // the next unused event of the pool (a follow mark reuses its predecessor's event)
+  const size_t k = ctx->tm_marks.empty() ? 0 : (size_t)ctx->tm_marks.back().first + 1;
   if (k == ctx->tm_pool.size()) {
     hipEvent_t e;
     // timing only (resolved after a stream synchronisation): no system-scope fence on
