@@ -60,7 +60,6 @@ void refresh_state(bann_ctx* ctx) {
   s.pred = ctx->d_pred;
   s.pred0 = ctx->d_pred0;
   s.scr = ctx->d_scr;
-  s.foldq = ctx->d_foldq;
   s.dbg = ctx->d_dbg;
   s.eprec = ctx->d_eprec;
   s.h0 = ctx->d_h0;
@@ -252,8 +251,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       grp->items.push_back(it);
     }
     if (solo) {
-      p.fold.push_back(FoldJob{b, ns * spi, solo_part, solo_rss,
-                               (int64_t)p.fold.size() * 8 * ctx->max_p_fused});
+      p.fold.push_back(FoldJob{b, ns * spi, solo_part, solo_rss});
       solo_part += (int64_t)ns * spi * h.P;
       solo_rss += (int64_t)ns * spi;
     }
@@ -500,7 +498,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
                   ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_fold_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
-                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt, ctx->d_foldq,
+                  ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt,
                   ctx->d_res_part};
   for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
   clear_graphs(ctx);
@@ -1017,11 +1015,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(hipMemsetAsync(ctx->d_pred0, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_scr, scr_off));
   CK(dalloc(&ctx->d_eprec, nb));
-  CK(dalloc(&ctx->d_upd_cnt, nb * UPD_CNT_STRIDE));
-  CK(hipMemsetAsync(ctx->d_upd_cnt, 0, nb * UPD_CNT_STRIDE * sizeof(int32_t), ctx->stream));
-  // the fused solo fold's group sums: a solo plan has < solo_threshold (<= cus) branches
-  ctx->max_p_fused = max_p_fused;
-  CK(dalloc(&ctx->d_foldq, std::max<int64_t>(1, (int64_t)cus * 8 * max_p_fused)));
+  CK(dalloc(&ctx->d_upd_cnt, nb));
+  CK(hipMemsetAsync(ctx->d_upd_cnt, 0, nb * sizeof(int32_t), ctx->stream));
   CK(dalloc(&ctx->d_u, nb));
   CK(dalloc(&ctx->d_h0, nb));
   CK(dalloc(&ctx->d_ld, nb));

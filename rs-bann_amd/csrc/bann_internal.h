@@ -82,12 +82,7 @@ struct FoldJob {
   int32_t nslab;
   int64_t part;
   int64_t rss;
-  int64_t vq;  // fused tail (kernels_fx.hip): the branch's 8 group sums v_q in DevState::foldq
 };
-// per-branch arrival counters of the fused update (DevState-independent, zero between
-// launches): [0] the branch's workgroups (multi-split plans), [1 + q] the slabs of fold
-// group q (solo plans), [9] the fold groups
-#define UPD_CNT_STRIDE 10
 
 // Per-branch derived constants of the fused path (rewritten after every position update).
 struct FusedConst {
@@ -116,7 +111,6 @@ struct DevState {
   float* pred;            // predictions [nbranch][n]
   float* pred0;           // predictions at the trajectory start
   float* scr;             // gx-path scratch (one scratch group's worth)
-  float* foldq;           // fused solo fold: per fold job 8 group sums of P floats
   float* eprec;           // error precision per branch
   double* h0;             // initial -H per branch
   double* htrace;         // [nbranch][Lint+1]

@@ -87,9 +87,7 @@ struct bann_ctx {
   uint8_t* d_xi = nullptr;   // individual-major 2-bit images of the fx branches (kernels_fi.hip; BANN_FWD_FI=0: none)
   int64_t xi_bytes = 0;
   int32_t cus = 256;
-  int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update ([nbranch][UPD_CNT_STRIDE])
-  float* d_foldq = nullptr;        // the fused solo fold's group sums (DevState::foldq)
-  int64_t max_p_fused = 0;
+  int32_t* d_upd_cnt = nullptr;  // per-branch arrival counters of the fused update (zero between launches)
   // the update in the gradient launch's tail (BANN_FUSE_UPDATE=1; same bits either way):
   // one-split plans (the branch's one workgroup), one-round multi-split plans and solo
   // plans (the last arriving workgroup; solo: it folds the branch's slabs first).  Off

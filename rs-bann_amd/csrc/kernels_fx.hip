@@ -573,74 +573,27 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // arrival (agent scope), and the last arriver acquires before reading the slabs.
     __shared__ int s_last;
     __shared__ double s_redd[4 * 8];
-    double* const s_rsv = reinterpret_cast<double*>(&s_x[1][0][0]);  // 256 doubles in a free tile slot
-    int32_t* const cb = upd_cnt + (int64_t)UPD_CNT_STRIDE * b;
-    // one lane counts an arrival on counter c (expected n arrivals in all) after every
-    // wave has drained its write-through stores; the last arriver acquires the others'
-    auto arrive_last = [&](int c, int n) -> bool {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        s_last = __hip_atomic_fetch_add(&cb[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
-        if (s_last) {
+    if (pub) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int narr = folds ? folds[it.fold_ix].nslab : bd.nsplits;
+    if (threadIdx.x == 0)
+      s_last = !pub || __hip_atomic_fetch_add(&upd_cnt[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == narr - 1;
+    __syncthreads();
+    if (s_last) {
+      if (pub) {
+        if (threadIdx.x == 0) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          cb[c] = 0;  // for the next launch (ordered by the kernel boundary)
+          upd_cnt[b] = 0;  // for the next launch (ordered by the kernel boundary)
         }
+        __syncthreads();
       }
-      __syncthreads();
-      return s_last != 0;
-    };
-    float* s_th = reinterpret_cast<float*>(&s_x[0][0][0]);  // the tile slots are free: P <= 2048 floats
-    if (!pub) {
-      __syncthreads();  // one split: this workgroup's own slab, visible to its waves after a barrier
+      if (folds) {
+        fold_solo_all<64 * FX_WAVES>(st, folds[it.fold_ix], bd);
+        __syncthreads();  // slab 0 and its rss, written by this workgroup, read by update_small
+      }
+      float* s_th = reinterpret_cast<float*>(&s_x[0][0][0]);  // the tile slots are free: P <= 2048 floats
       update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
-    } else if (!folds) {
-      if (arrive_last(0, bd.nsplits))
-        update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
-    } else {
-      // solo plan: k_fold_solo's sums in two levels.  Slab s belongs to group q = s mod 8;
-      // the last arriving workgroup of group q adds its slabs in increasing s (k_fold_solo's
-      // v_q), the last of the groups adds v_0 + ... + v_7 into the branch's slab 0, folds
-      // the rss partials in slab order, and updates the branch
-      const FoldJob fj = folds[it.fold_ix];
-      const int P = bd.P, q = it.split & 7;
-      const int nq = (fj.nslab - q + 7) >> 3, ngrp = fj.nslab < 8 ? fj.nslab : 8;
-      const float* src = st.part + fj.part;
-      float* vq = st.foldq + fj.vq;
-      if (arrive_last(1 + q, nq)) {
-        for (int i = threadIdx.x; i < P; i += 64 * FX_WAVES) {
-          float v = 0.f;
-          for (int s2 = q; s2 < fj.nslab; s2 += 8) v += src[(int64_t)s2 * P + i];
-          __hip_atomic_store(vq + (int64_t)q * P + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (arrive_last(9, ngrp)) {
-          float* dst = st.part + bd.part_off;
-          for (int i = threadIdx.x; i < P; i += 64 * FX_WAVES) {
-            float t = vq[i];
-#pragma unroll
-            for (int k = 1; k < 8; ++k) t += k < ngrp ? vq[(int64_t)k * P + i] : 0.f;
-            dst[i] = t;
-            for (int s2 = 1; s2 < bd.nsplits; ++s2) dst[(int64_t)s2 * P + i] = 0.f;
-          }
-          // rss: the slabs' partials in slab order (gathered by all lanes, added by one)
-          double r = 0.0;
-          for (int s0 = 0; s0 < fj.nslab; s0 += 256) {
-            __syncthreads();
-            if (s0 + (int)threadIdx.x < fj.nslab) s_rsv[threadIdx.x] = st.rss_part[fj.rss + s0 + threadIdx.x];
-            __syncthreads();
-            if (threadIdx.x == 0)
-              for (int k = 0; k < 256 && s0 + k < fj.nslab; ++k) r += s_rsv[k];
-          }
-          if (threadIdx.x == 0) {
-            double* rd = st.rss_part + (int64_t)b * st.max_splits;
-            rd[0] = r;
-            for (int s2 = 1; s2 < bd.nsplits; ++s2) rd[s2] = 0.0;
-          }
-          __syncthreads();  // slab 0 and its rss, written by this workgroup, read by update_small
-          update_small<64 * FX_WAVES, 1, 2>(st, b, bd, upd_mode, false, upd_step, s_redd, s_th);
-        }
-      }
     }
   }
 }
