@@ -126,7 +126,10 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
 // NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
 // so the LDS reads of a whole phase issue back to back); 0 = any count <= 8.
 
-template <int NL, int ACT, int NCH>
+// UPD: the instantiation with the fused update tail (bann_api.hip fuse_update plans);
+// the default one carries no tail code at all (its registers: the tail's live values
+// made the tile loop spill scalar registers to vector lanes)
+template <int NL, int ACT, int NCH, int UPD>
 __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     k_fused_grad_fx(DevState st, const GradItem* __restrict__ items, int write_pred, int upd_mode, int upd_step,
                     int32_t* __restrict__ upd_cnt, const FoldJob* __restrict__ folds) {
@@ -508,7 +511,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   // a fused update with more than one workgroup per branch: the partials are handed
   // to the branch's last arriving workgroup inside the launch, stored write-through
   // (sc1: no release fence needed; MI355X_MICROARCH.md, inter-workgroup visibility)
-  const bool pub = upd_cnt != nullptr && (folds != nullptr || bd.nsplits > 1);
+  const bool pub = UPD && upd_cnt != nullptr && (folds != nullptr || bd.nsplits > 1);
   auto pst = [&](float* a, float v) {
     if (pub)
       __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -562,7 +565,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     else
       st.rss_part[it.rss_at] = rs;
   }
-  if (upd_cnt) {
+  if constexpr (UPD) {
     // fused leapfrog update (bann_api.hip build_plan): the last of the branch's
     // workgroups to finish updates it here, with the update kernel's arithmetic and
     // reduction order (update_small as 512 virtual threads), instead of a second
@@ -598,17 +601,25 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   }
 }
 
+template <int NL, int NCH, int UPD>
+static void launch_fx_nlu(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, int um, int us,
+                          int32_t* cnt, const FoldJob* fo, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
+  switch (act) {
+    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH, UPD>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH, UPD>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH, UPD>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH, UPD>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH, UPD>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
+  }
+}
 template <int NL, int NCH>
 static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int wp, int um, int us,
                          int32_t* cnt, const FoldJob* fo, hipStream_t s) {
-  const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
-  switch (act) {
-    case 0: hipLaunchKernelGGL((k_fused_grad_fx<NL, 0, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
-    case 1: hipLaunchKernelGGL((k_fused_grad_fx<NL, 1, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
-    case 2: hipLaunchKernelGGL((k_fused_grad_fx<NL, 2, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
-    case 3: hipLaunchKernelGGL((k_fused_grad_fx<NL, 3, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
-    default: hipLaunchKernelGGL((k_fused_grad_fx<NL, 4, NCH>), grid, block, 0, s, st, items, wp, um, us, cnt, fo); break;
-  }
+  if (cnt)
+    launch_fx_nlu<NL, NCH, 1>(st, items, nitems, act, wp, um, us, cnt, fo, s);
+  else
+    launch_fx_nlu<NL, NCH, 0>(st, items, nitems, act, wp, um, us, nullptr, nullptr, s);
 }
 
 // full8: every branch of this launch group has exactly 8 chunks; upd_cnt != null:
