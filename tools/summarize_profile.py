@@ -51,15 +51,17 @@ for r in timed:
     per_kernel.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 
 
-def pmc_bytes(sub, counter, pick=statistics.median):
+def pmc_bytes(sub, counter, pick=statistics.median, kernel="k_fused_grad"):
     f = find(sub, "*counter_collection.csv")
     rows = list(csv.DictReader(open(f)))
     per = {}
     for r in rows:
-        if "k_fused_grad" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             key = r.get("Dispatch_Id") or r.get("Correlation_Id")
             per.setdefault(key, [int(r["Grid_Size"]) if "Grid_Size" in r else 0, 0.0])
             per[key][1] += float(r["Counter_Value"])
+    if not per:
+        return None
     vals = [v for g, v in per.values()]
     gmax = max(g for g, v in per.values())
     vals = [v for g, v in per.values() if g == gmax]
@@ -71,6 +73,13 @@ fetch = pmc_bytes("fetch", "FETCH_SIZE") * 2.0   # gfx950: FETCH_SIZE counts 1/2
 # last launch of a trajectory also write the n predictions per branch (4 n B)
 write = pmc_bytes("write", "WRITE_SIZE", min)
 write_pred = pmc_bytes("write", "WRITE_SIZE", max)
+# the network sampler's forward-only launch (k_forward_fx / k_forward_fi), when the command ran one
+fwd_fetch = None
+for fk in ("k_forward_fx", "k_forward_fi"):
+    fb = pmc_bytes("fetch", "FETCH_SIZE", kernel=fk)
+    if fb is not None:
+        fwd_fetch = (fk, fb * 2.0)
+        break
 pmc = {"kernel": full[0]["Kernel_Name"], "config": bench["config"]["workload"],
        "timed_trajectory_grad_ms_mean": statistics.mean(tgrad) if tgrad else None,
        "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
@@ -135,6 +144,14 @@ with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
     f.write(f"HBM traffic per gradient launch (PMC): fetch {fetch/1e9:.3f} GB, write {write/1e9:.4f} GB "
             f"({write_pred/1e9:.4f} GB at a trajectory's first/last launch, predictions included); "
             f"algorithmic {pmc['alg_bytes_per_launch']/1e9:.3f} GB\n\n")
+    if fwd_fetch is not None:
+        xb = bench["roofline"]["alg_bytes_per_launch"] - 4 * int(bench["config"]["n"]) * (
+            1 if "network error once" in bench["roofline"].get("alg_bytes_basis", "") else int(bench["config"]["branches_per_gpu"]))
+        fmean = statistics.mean(next(v for k, v in per_kernel.items() if fwd_fetch[0] in k)) if any(fwd_fetch[0] in k for k in per_kernel) else None
+        f.write(f"Forward-only launch ({fwd_fetch[0]}, PMC): fetch {fwd_fetch[1]/1e9:.3f} GB per launch against "
+                f"{xb/1e9:.3f} GB of 2-bit genotypes"
+                + (f"; timed-trajectory mean {fmean:.4f} ms = {xb / (fmean * 1e-3) / 1e9:.0f} GB/s = "
+                   f"{xb / (fmean * 1e-3) / 8e12:.3f} of 8 TB/s" if fmean else "") + "\n\n")
     f.write(f"achieved (algorithmic bytes / median launch): "
             f"{pmc['alg_bytes_per_launch'] / (statistics.median(dur) * 1e-3) / 1e9:.0f} GB/s\n\n")
     if "mfma" in pmc:
