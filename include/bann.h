@@ -186,6 +186,18 @@ int bann_log_density_gradient_joint(bann_ctx* ctx, int32_t b, const float* hyper
  * pre-activations of the hidden and summary layers (the output's equals its
  * activation and is not repeated), sum_{l<L-1} w_l n floats. */
 int bann_forward_feed(bann_ctx* ctx, int32_t b, float* pre_out, float* act_out);
+/* BranchSampler::effect_sizes (branch_sampler.rs:784-811): the n x m matrix of
+ * branch b at its current parameters, column-major (element (i, j) at j n + i).
+ * As the reference: the backward chain is seeded with the branch output times
+ * W_out^T (792-797), not with the error (so entry (i, j) is out_i d out_i / d x_ij),
+ * and no absolute value is taken (the doc comment says "absolute values"; the
+ * code does not). */
+int bann_effect_sizes(bann_ctx* ctx, int32_t b, float* out);
+/* the per-branch part of Net::population_effect_sizes (net.rs:529-543): for
+ * each listed branch the column means sum_i effect_sizes(i, j) / n, m_b floats
+ * per branch, concatenated in list order.  The sum over individuals is taken
+ * through the layer-0 deltas (sum_j W0(j,k) sum_i delta0(i,k)), in f64. */
+int bann_population_effect_sizes(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* out);
 /* log_density (branch_sampler.rs:72-78; std_normal_branch.rs:149-158) at the
  * current parameters and the given rss */
 int bann_log_density(bann_ctx* ctx, int32_t b, double rss, double* out);

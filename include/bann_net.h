@@ -70,6 +70,9 @@ typedef struct {
   int32_t gradient_descent_joint;  /* MCMCCfg::gradient_descent_joint: gradient_descent_joint (1019-1066), L
                                       ascent steps of params and precisions at the step size factor, no Gibbs
                                       draws; rejected if the error precision ends <= 0 */
+  int32_t effect_sizes;  /* MCMCCfg::effect_sizes (mcmc_cfg.rs:29): after burn-in, every branch update
+                            writes outdir/effect_sizes/<chain_ix>_<branch_ix>, the n x m effect_sizes
+                            of the branch as CSV (net.rs:307-315, 458-465, 571-587) */
 } bann_mcmc_cfg;
 
 /* Host random source for the driver's draws (the reference's ThreadRng,
@@ -161,6 +164,10 @@ int bann_net_branch_r2s(bann_net* net, bann_ctx* ctx, const float* y, int64_t n,
 /* Net::activations (net.rs:509-518) of branch b: forward_feed's activations of
  * every layer at the net's parameters (bann_forward_feed layout); ctx as above */
 int bann_net_activations(bann_net* net, bann_ctx* ctx, int32_t b, float* act_out);
+/* Net::population_effect_sizes (net.rs:529-543): per branch, in branch order, the
+ * mean over the individuals of ctx's cohort of effect_sizes (branch_sampler.rs:784-811)
+ * at the net's parameters: sum_b m_b floats; ctx as above */
+int bann_net_population_effect_sizes(bann_net* net, bann_ctx* ctx, float* out);
 int bann_net_summary(const bann_net* net, bann_train_summary* out);
 /* the recorded mse_train / lpd series (TrainingStats::mse_train / lpd);
  * writes min(cap, num_records) entries of each (either may be NULL) */

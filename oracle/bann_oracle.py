@@ -215,6 +215,26 @@ def backpropagate(br: Branch, X: np.ndarray, y: np.ndarray):
     return rss_v, dW, db
 
 
+def effect_sizes(br: Branch, X: np.ndarray) -> np.ndarray:
+    """branch_sampler.rs:784-811: out_i d out_i / d x_ij per individual and marker (n x m).
+
+    As the reference computes it: the chain is seeded with the branch OUTPUT
+    times W_out^T (792-797), not with the error, and no absolute value is taken
+    (the doc comment says "absolute values"; the code does not)."""
+    L = br.num_layers
+    pre, acts = forward_feed(br, X)                                   # 789
+    err = acts[-1] @ br.weights[L - 1].T                              # 792-797
+    for l in range(L - 2, -1, -1):                                    # 799-808
+        delta = dhdx(pre[l], br.act) * err
+        err = delta @ br.weights[l].T
+    return err
+
+
+def population_effect_sizes(branches: Sequence[Branch], Xs: Sequence[np.ndarray]) -> np.ndarray:
+    """net.rs:529-543: per branch the column sums of effect_sizes / n, concatenated."""
+    return np.concatenate([effect_sizes(br, X).sum(axis=0) / X.shape[0] for br, X in zip(branches, Xs)])
+
+
 # --------------------------------------------------------------------------
 # priors: log density and gradient w.r.t. weights
 # --------------------------------------------------------------------------

@@ -54,7 +54,7 @@ class McmcCfg(C.Structure):
                 ("chain_length", C.c_int32), ("burn_in", C.c_int32), ("fixed_param_precisions", C.c_int32),
                 ("sampled_output_bias", C.c_int32), ("trace", C.c_int32), ("trajectories", C.c_int32),
                 ("joint_hmc", C.c_int32), ("gradient_descent", C.c_int32),
-                ("gradient_descent_joint", C.c_int32)]
+                ("gradient_descent_joint", C.c_int32), ("effect_sizes", C.c_int32)]
 
 
 # bann_allreduce_fn: in-place sum over ranks of a host buffer (dtype 0 f32, 1 f64)
@@ -114,6 +114,8 @@ SIGNATURES = {
     "bann_log_density_gradient_many": (C.c_int, [_P, _pi32, _i32, _pf32, _pf64]),
     "bann_log_density_gradient_joint": (C.c_int, [_P, _i32, _pf32, _pf32, _pf64, _pf64]),
     "bann_forward_feed": (C.c_int, [_P, _i32, _pf32, _pf32]),
+    "bann_effect_sizes": (C.c_int, [_P, _i32, _pf32]),
+    "bann_population_effect_sizes": (C.c_int, [_P, _pi32, _i32, _pf32]),
     "bann_neg_hamiltonian": (C.c_int, [_P, _i32, _pf32, _pf64]),
     "bann_hmc_step": (C.c_int, [_P, _pi32, _i32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32, _pi32, _pf64,
                                 _pi32, _pf64]),
@@ -171,6 +173,7 @@ SIGNATURES = {
     "bann_net_gradient": (C.c_int, [_P, _P, _pf32, _i64, _pf32]),
     "bann_net_branch_r2s": (C.c_int, [_P, _P, _pf32, _i64, _pf32]),
     "bann_net_activations": (C.c_int, [_P, _P, _i32, _pf32]),
+    "bann_net_population_effect_sizes": (C.c_int, [_P, _P, _pf32]),
     "bann_net_summary": (C.c_int, [_P, C.POINTER(TrainSummary)]),
     "bann_net_records": (C.c_int, [_P, _pf32, _pf32, _i32]),
     "bann_net_residual": (C.c_int, [_P, _pf32]),

@@ -247,6 +247,23 @@ class BannContext:
             return out
         return (split(pr, widths[:-1]) if pre else None), split(act, widths)
 
+    def effect_sizes(self, b: int) -> np.ndarray:
+        """BranchSampler::effect_sizes (branch_sampler.rs:784-811): the [n, m] matrix
+        out_i d out_i / d x_ij at the branch's current parameters (output-seeded chain, no abs)."""
+        m = self.branch_info(b)[0]
+        out = np.zeros(m * self.n, np.float32)
+        self._check(self._lib.bann_effect_sizes(self._h, b, _ptr(out, C.c_float)))
+        return out.reshape(m, self.n).T
+
+    def population_effect_sizes(self, branches) -> np.ndarray:
+        """the per-branch column means of effect_sizes (Net::population_effect_sizes,
+        net.rs:529-543), concatenated in list order."""
+        bl = np.ascontiguousarray(branches, dtype=np.int32)
+        out = np.zeros(sum(self.branch_info(int(b))[0] for b in bl), np.float32)
+        self._check(self._lib.bann_population_effect_sizes(self._h, _ptr(bl, C.c_int32), bl.size,
+                                                           _ptr(out, C.c_float)))
+        return out
+
     def branch_info(self, b: int):
         """(markers, num_layers, layer widths, activation code, prior code) of branch b."""
         m, L, act, pr = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()

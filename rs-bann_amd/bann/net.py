@@ -39,6 +39,7 @@ class MCMCConfig:
     joint_hmc: bool = False      # hmc_step_joint over params and precisions, no Gibbs draws (net.rs:270-290)
     gradient_descent: bool = False        # BranchSampler::gradient_descent (line search, branch_sampler.rs:964-1016)
     gradient_descent_joint: bool = False  # gradient_descent_joint (params and precisions, 1019-1066)
+    effect_sizes: bool = False   # outdir/effect_sizes/<chain_ix>_<branch_ix> CSVs after burn-in (net.rs:307-315)
 
     def to_c(self) -> McmcCfg:
         burn = self.chain_length - 1 if self.burn_in is None else self.burn_in
@@ -46,7 +47,7 @@ class MCMCConfig:
                        STEP_MODES[self.hmc_step_size_mode], self.chain_length, max(burn, 0),
                        int(self.fixed_param_precisions), int(self.sampled_output_bias), int(self.trace),
                        int(self.trajectories), int(self.joint_hmc), int(self.gradient_descent),
-                       int(self.gradient_descent_joint))
+                       int(self.gradient_descent_joint), int(self.effect_sizes))
 
 
 class Net:
@@ -165,6 +166,15 @@ class Net:
             res.append(out[o: o + w * c.n].reshape(w, c.n).T)
             o += w * c.n
         return res
+
+    def population_effect_sizes(self, ctx=None) -> np.ndarray:
+        """Net::population_effect_sizes (net.rs:529-543): per branch (branch order) the mean over
+        ctx's individuals of effect_sizes (branch_sampler.rs:784-811), concatenated."""
+        c = ctx if ctx is not None else self._ctx
+        out = np.zeros(sum(c.branch_info(b)[0] for b in range(c.num_branches)), np.float32)
+        self._check(self._lib.bann_net_population_effect_sizes(self._h, self._ctxh(ctx),
+                                                               out.ctypes.data_as(C.POINTER(C.c_float))))
+        return out
 
     def summary(self) -> dict:
         s = TrainSummary()

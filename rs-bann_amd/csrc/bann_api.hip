@@ -1355,6 +1355,85 @@ extern "C" int bann_forward_feed(bann_ctx* ctx, int32_t b, float* pre_out, float
   return BANN_OK;
 }
 
+namespace {
+// device scratch of the effect-size chain, sized for the largest listed branch
+struct EffectScratch {
+  float *pre = nullptr, *act = nullptr, *ea = nullptr, *eb = nullptr, *full = nullptr, *pop = nullptr;
+  double* s = nullptr;
+  ~EffectScratch() {
+    dfree(pre);
+    dfree(act);
+    dfree(ea);
+    dfree(eb);
+    dfree(full);
+    dfree(pop);
+    dfree(s);
+  }
+  hipError_t alloc(const bann_ctx* ctx, const int32_t* branches, int32_t nb, bool want_full) {
+    int64_t wp = 1, wa = 1, we = 1, wm = 1, w0 = 1;
+    for (int32_t i = 0; i < nb; ++i) {
+      const BranchHost& h = ctx->br[branches[i]];
+      int64_t p = 0, a = 0;
+      for (int l = 0; l < h.L; ++l) {
+        a += h.widths[l];
+        if (l < h.L - 1) p += h.widths[l];
+        if (l >= 1) we = std::max<int64_t>(we, h.dev.win[l]);
+      }
+      wp = std::max(wp, p);
+      wa = std::max(wa, a);
+      wm = std::max<int64_t>(wm, h.m);
+      w0 = std::max<int64_t>(w0, h.widths[0]);
+    }
+    const int64_t n = ctx->n;
+    hipError_t e = dalloc(&pre, wp * n);
+    if (e == hipSuccess) e = dalloc(&act, wa * n);
+    if (e == hipSuccess) e = dalloc(&ea, we * n);
+    if (e == hipSuccess) e = dalloc(&eb, we * n);
+    if (e == hipSuccess) e = want_full ? dalloc(&full, wm * n) : dalloc(&pop, wm);
+    if (e == hipSuccess) e = dalloc(&s, w0);
+    return e;
+  }
+};
+}  // namespace
+
+// BranchSampler::effect_sizes (branch_sampler.rs:784-811): forward_feed + the
+// output-seeded backward chain (kernels_feed.hip), the n x m matrix to the host
+extern "C" int bann_effect_sizes(bann_ctx* ctx, int32_t b, float* out) {
+  if (!check_branch(ctx, b) || !out) return fail(ctx, BANN_E_ARG, "bad branch or null output");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  const BranchHost& h = ctx->br[b];
+  EffectScratch sc;
+  if (sc.alloc(ctx, &b, 1, true) != hipSuccess) return fail(ctx, BANN_E_OOM, "effect_sizes scratch");
+  launch_forward_feed(ctx->st, b, h.dev, sc.pre, sc.act, ctx->stream);
+  launch_effect_sizes(ctx->st, b, h.dev, sc.pre, sc.act, sc.ea, sc.eb, sc.full, nullptr, nullptr, ctx->stream);
+  CK(hipGetLastError());
+  CK(hipMemcpyAsync(out, sc.full, (int64_t)h.m * ctx->n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
+// Net::population_effect_sizes' per-branch column means (net.rs:529-543)
+extern "C" int bann_population_effect_sizes(bann_ctx* ctx, const int32_t* branches, int32_t nb, float* out) {
+  if (!ctx || !branches || nb <= 0 || !out) return fail(ctx, BANN_E_ARG, "null pointer or empty branch list");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  for (int32_t i = 0; i < nb; ++i)
+    if (!check_branch(ctx, branches[i])) return fail(ctx, BANN_E_ARG, "bad branch index");
+  EffectScratch sc;
+  if (sc.alloc(ctx, branches, nb, false) != hipSuccess) return fail(ctx, BANN_E_OOM, "population_effect_sizes scratch");
+  int64_t at = 0;
+  for (int32_t i = 0; i < nb; ++i) {
+    const BranchHost& h = ctx->br[branches[i]];
+    launch_forward_feed(ctx->st, branches[i], h.dev, sc.pre, sc.act, ctx->stream);
+    launch_effect_sizes(ctx->st, branches[i], h.dev, sc.pre, sc.act, sc.ea, sc.eb, nullptr, sc.s, sc.pop,
+                        ctx->stream);
+    CK(hipGetLastError());
+    CK(hipMemcpyAsync(out + at, sc.pop, (int64_t)h.m * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    at += h.m;
+  }
+  CK(hipStreamSynchronize(ctx->stream));
+  return BANN_OK;
+}
+
 // host evaluation of log_density at the current parameters (branch_sampler.rs:72-78)
 static int host_log_density(bann_ctx* ctx, int32_t b, double rss, double* out) {
   const BranchHost& h = ctx->br[b];

@@ -220,5 +220,9 @@ void launch_snapshot_pred(const DevState& st, const int32_t* branches, int32_t n
 int64_t residual_delta_scratch_floats(int64_t n);
 // forward_feed with every layer (kernels_feed.hip): pre [sum_{l<L-1} w_l][n] (may be null), act [sum_l w_l][n]
 void launch_forward_feed(const DevState& st, int b, const BranchDev& bd, float* pre, float* act, hipStream_t s);
+// effect_sizes over forward_feed's layers: ea / eb two [max w_l][n] buffers; full [m][n] and / or
+// pop [m] (column means, s: w_0 doubles of scratch); either may be null
+void launch_effect_sizes(const DevState& st, int b, const BranchDev& bd, const float* pre, const float* act,
+                         float* ea, float* eb, float* full, double* s, float* pop, hipStream_t strm);
 void launch_residual_delta(const DevState& st, const int32_t* branches, int32_t nb, float* scratch, float* out,
                            hipStream_t s);

@@ -455,6 +455,82 @@ int append_text(bann_net* t, const std::string& path, const std::string& text) {
   return (std::fclose(f) == 0 && ok) ? BANN_OK : fail(t, BANN_E_ARG, "short write to " + path);
 }
 
+// Rust's Display of an f32 (f32::to_string, as net.rs:584 writes the effect
+// sizes): the shortest decimal that reads back to the same f32 (the closest of
+// them if several), printed positionally -- no exponent, no trailing ".0"
+// ("1", "0.1", "0.0000001", "100000000000000000000"), "-0", "NaN", "inf".
+void rust_f32(std::string& o, float v) {
+  if (std::isnan(v)) {
+    o += "NaN";
+    return;
+  }
+  if (std::signbit(v)) o += '-';
+  const float a = std::fabs(v);
+  if (std::isinf(a)) {
+    o += "inf";
+    return;
+  }
+  if (a == 0.f) {
+    o += '0';
+    return;
+  }
+  char buf[48];
+  std::string dig;
+  int e10 = 0;
+  for (int p = 0; p < 9; ++p) {  // p + 1 significant digits; 9 always round-trip
+    std::snprintf(buf, sizeof(buf), "%.*e", p, (double)a);
+    char* ep = std::strchr(buf, 'e');
+    std::string d(buf, ep);
+    const int ex = std::atoi(ep + 1);
+    d.erase(std::remove(d.begin(), d.end(), '.'), d.end());
+    auto reads_back = [&](const std::string& s) {
+      std::snprintf(buf, sizeof(buf), "%s.%se%d", s.substr(0, 1).c_str(), s.substr(1).c_str(), ex);
+      return std::strtof(buf, nullptr) == a;
+    };
+    if (reads_back(d)) {
+      dig = d;
+      e10 = ex;
+      break;
+    }
+    // the correctly rounded p+1 digits miss, a neighbour of the same length may not
+    // (asymmetric rounding intervals at powers of two): take the closer one that reads back
+    std::string best;
+    double bd = 0.0;
+    for (int s = -1; s <= 1; s += 2) {
+      long long q = std::atoll(d.c_str()) + s;
+      std::string c = std::to_string(q);
+      if ((int)c.size() != p + 1) continue;
+      if (reads_back(c)) {
+        std::snprintf(buf, sizeof(buf), "%s.%se%d", c.substr(0, 1).c_str(), c.substr(1).c_str(), ex);
+        const double dist = std::fabs(std::strtod(buf, nullptr) - (double)a);
+        if (best.empty() || dist < bd) {
+          best = c;
+          bd = dist;
+        }
+      }
+    }
+    if (!best.empty()) {
+      dig = best;
+      e10 = ex;
+      break;
+    }
+  }
+  while (dig.size() > 1 && dig.back() == '0') dig.pop_back();
+  const int k = (int)dig.size(), pt = e10 + 1;  // value = 0.dig x 10^pt
+  if (pt <= 0) {
+    o += "0.";
+    o.append((size_t)(-pt), '0');
+    o += dig;
+  } else if (pt < k) {
+    o += dig.substr(0, pt);
+    o += '.';
+    o += dig.substr(pt);
+  } else {
+    o += dig;
+    o.append((size_t)(pt - k), '0');
+  }
+}
+
 bool mkdir_p(const std::string& d) {
   if (d.empty()) return true;
   std::string cur;
@@ -465,6 +541,32 @@ bool mkdir_p(const std::string& d) {
     }
   }
   return true;
+}
+
+// Net::save_effect_sizes (net.rs:571-587): effect_sizes of branch b (n x m, the
+// device chain of bann_effect_sizes) as CSV at dir/effect_sizes/<chain_ix>_<b>:
+// one row per individual, one field per marker (transpose + chunks(m) of the
+// column-major matrix), csv::Writer defaults (',' and "\n", numbers unquoted)
+int save_effect_sizes(bann_net* t, int b, int chain_ix, const std::string& dir) {
+  const Branch& B = t->br[b];
+  const int64_t n = t->n, m = B.m;
+  std::vector<float> e((size_t)n * m);
+  CKB(bann_effect_sizes(t->ctx, b, e.data()));
+  const std::string path = dir + "/effect_sizes/" + std::to_string(chain_ix) + "_" + std::to_string(b);
+  FILE* f = std::fopen(path.c_str(), "w");
+  if (!f) return fail(t, BANN_E_ARG, "cannot open " + path);
+  std::string row;
+  bool ok = true;
+  for (int64_t i = 0; i < n && ok; ++i) {
+    row.clear();
+    for (int64_t j = 0; j < m; ++j) {
+      if (j) row += ',';
+      rust_f32(row, e[(size_t)j * n + i]);
+    }
+    row += '\n';
+    ok = std::fwrite(row.data(), 1, row.size(), f) == row.size();
+  }
+  return (std::fclose(f) == 0 && ok) ? BANN_OK : fail(t, BANN_E_ARG, "short write to " + path);
 }
 
 Writer serialize(const bann_net* t) {
@@ -744,7 +846,8 @@ int gradient_descent_joint(bann_net* t, int b, const bann_mcmc_cfg* cfg, double 
 // one branch update of Net::train / train_single_branch (net.rs:261-332): Gibbs
 // draws (unless joint), target = residual + f_b, the HMC trajectory on the
 // device, the residual bookkeeping on the device, global params, output bias
-int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const std::string& dir, Draws& dr) {
+int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const std::string& dir, Draws& dr,
+                  int chain_ix) {
   Branch& B = t->br[b];
   const int64_t n = t->n;
   const double kout = t->hp.output_shape, sout = t->hp.output_scale;
@@ -841,6 +944,11 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   t->g_eprec = B.prec[B.epoff];
   t->g_oprec = B.prec[B.out_prec_ix()];
   t->g_reg_sum = B.ows_reg_sum;
+  // net.rs:307-315 / 458-465: the branch's effect sizes after burn-in
+  if (cfg->effect_sizes && chain_ix >= cfg->burn_in && !dir.empty()) {
+    const int rc = save_effect_sizes(t, b, chain_ix, dir);
+    if (rc) return rc;
+  }
   // output bias (net.rs:319-332): residual += bias, draw, residual -= bias
   t->ob_eprec = t->g_eprec;
   CKB(bann_residual_shift(t->ctx, t->ob_bias, &sr, nullptr));
@@ -867,7 +975,9 @@ int train_begin(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg
     return fail(t, BANN_E_ARG, "step size mode: Izmailov, uniform or random (StdScaled is unusable in the reference)");
   if (n != bann_ctx_num_individuals(t->ctx)) return fail(t, BANN_E_SHAPE, "phenotype length differs from the cohort");
   t->n = n;
-  if (!dir.empty() && !mkdir_p(dir + "/models")) return fail(t, BANN_E_ARG, "cannot create " + dir + "/models");
+  // net.rs:208-211: the models and effect-size directories
+  if (!dir.empty() && (!mkdir_p(dir + "/models") || !mkdir_p(dir + "/effect_sizes")))
+    return fail(t, BANN_E_ARG, "cannot create the output directories under " + dir);
   // initialize_stats: residual = y - bias - sum_b f_b on the device (one packed forward for stale rows)
   for (auto& B : t->br) cfg_update_global(t, B);
   CKB(bann_residual_init(t->ctx, y, t->ob_bias, nullptr, &t->rss_cur));
@@ -934,7 +1044,7 @@ extern "C" int bann_net_train(bann_net* t, const float* y, int64_t n, const bann
       std::swap(order[i], order[j]);
     }
     for (int b : order)
-      if ((rc = update_branch(t, b, cfg, traj, dir, dr))) return rc;
+      if ((rc = update_branch(t, b, cfg, traj, dir, dr, chain_ix))) return rc;
     if ((rc = train_record(t, chain_ix, cfg, dir, trace))) return rc;
   }
   CKB(bann_set_trajectory_recording(t->ctx, 0));
@@ -952,7 +1062,7 @@ extern "C" int bann_net_train_single_branch(bann_net* t, const float* y, int64_t
   if (rc) return rc;
   Draws dr;
   for (int chain_ix = 1; chain_ix <= cfg->chain_length; ++chain_ix) {  // net.rs:412-502: branch 0 every time
-    if ((rc = update_branch(t, 0, cfg, traj, dir, dr))) return rc;
+    if ((rc = update_branch(t, 0, cfg, traj, dir, dr, chain_ix))) return rc;
     if ((rc = train_record(t, chain_ix, cfg, dir, trace))) return rc;
   }
   CKB(bann_set_trajectory_recording(t->ctx, 0));
@@ -1090,6 +1200,18 @@ extern "C" int bann_net_activations(bann_net* t, bann_ctx* ctx, int32_t b, float
   if (rc) return rc;
   rc = bann_forward_feed(c, b, nullptr, act_out);
   return rc < 0 ? fail(t, rc, std::string("activations: ") + bann_last_error(c)) : BANN_OK;
+}
+
+extern "C" int bann_net_population_effect_sizes(bann_net* t, bann_ctx* ctx, float* out) {
+  if (!t || !out) return BANN_E_ARG;
+  bann_ctx* c = ctx ? ctx : t->ctx;
+  int rc = load_cfgs(t, c, bann_ctx_num_individuals(c));
+  if (rc) return rc;
+  const int nb = (int)t->br.size();
+  std::vector<int32_t> all(nb);
+  for (int b = 0; b < nb; ++b) all[b] = b;
+  rc = bann_population_effect_sizes(c, all.data(), nb, out);
+  return rc < 0 ? fail(t, rc, std::string("population_effect_sizes: ") + bann_last_error(c)) : BANN_OK;
 }
 
 extern "C" int bann_net_set_test_data(bann_net* t, bann_ctx* test_ctx, const float* y_test, int64_t n_test) {
