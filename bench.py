@@ -428,9 +428,9 @@ def main():
         wd.cancel()
         if rank == 0:
             log(json.dumps({"network_check": netcheck}))
-        if netcheck["status"] != "accepted":   # back at theta_0: the sweep-start targets again
-            ctx.residual_set(noise.astype(np.float32))
-            ctx.rebuild_targets(branches)
+        # the library leaves every branch's target at its Gibbs target of the state the
+        # check ended in (accepted: its last step; otherwise theta_0) and the device
+        # residual at y - sum_b f_b (include/bann.h): the branch line samples from there
 
     # warmup: a full trajectory of W steps (loads every kernel), then the
     # roofline's back-to-back launch timing (bann_profile_session: a 2-step

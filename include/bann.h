@@ -394,8 +394,10 @@ int bann_exchange_residual_device(bann_ctx* ctx);
  *   shared with every rank through the -H all-reduce, so all ranks decide alike.
  * Per step the first pass over the genotypes is forward-only (the outputs the
  * all-reduce needs); the gradient pass follows once e is known.
- * Outputs (may be NULL): status, h_trace[L+1], rss of the final state.  The
- * branch targets are left as the network targets f_b - e of the last step. */
+ * Outputs (may be NULL): status, h_trace[L+1], rss of the final state.  On
+ * return (accepted: theta_L, otherwise theta_0) every local branch's target is
+ * its Gibbs target y_b = f_b - e = y - bias - sum_{c != b} f_c over all ranks
+ * (net.rs:279-280), and the context's device residual is y - bias - sum_b f_b. */
 int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
                           float max_hamiltonian_error, int32_t step_mode, float step_factor, const float* eps,
                           const float* momentum, uint64_t seed, const float* u, int32_t* status_out,
@@ -421,6 +423,8 @@ int bann_set_hidden_gemm_bf16(bann_ctx* ctx, int32_t enabled);
  * bann_hmc_step (1) or launch kernel by kernel (0; default, or BANN_HMC_GRAPH);
  * the same launches, the same bits.  Trajectory recording always launches. */
 int bann_set_graph_replay(bann_ctx* ctx, int32_t enabled);
+/* the current graph-replay setting (0 / 1), or a negative status */
+int bann_get_graph_replay(const bann_ctx* ctx);
 /* force every branch onto the layered gx path (0) or allow the fused kernels (1) */
 int bann_set_fused_enabled(bann_ctx* ctx, int32_t enabled);
 /* bytes of packed genotype data read per full gradient evaluation of all branches */

@@ -183,6 +183,7 @@ SIGNATURES = {
     "bann_branch_get_trajectory": (C.c_int, [_P, _i32, _i32, _pi32, _pf32, _pf32, _pf64]),
     "bann_branch_get_trajectory_joint": (C.c_int, [_P, _i32, _i32, _pi32, _pf32, _pf32, _pf32, _pf64]),
     "bann_set_graph_replay": (C.c_int, [_P, _i32]),
+    "bann_get_graph_replay": (C.c_int, [_P]),
     "bann_net_save": (C.c_int, [_P, C.c_char_p]),
     "bann_net_load": (C.c_int, [_P, C.c_char_p]),
     "bann_net_last_error": (C.c_char_p, [_P]),

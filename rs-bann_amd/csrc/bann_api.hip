@@ -734,6 +734,7 @@ extern "C" int bann_set_graph_replay(bann_ctx* ctx, int32_t enabled) {
   ctx->graph_replay = enabled != 0;
   return BANN_OK;
 }
+extern "C" int bann_get_graph_replay(const bann_ctx* ctx) { return ctx ? (ctx->graph_replay ? 1 : 0) : BANN_E_ARG; }
 extern "C" int64_t bann_packed_genotype_bytes(const bann_ctx* ctx) { return ctx ? ctx->packed_bytes : 0; }
 
 extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
@@ -1569,7 +1570,7 @@ static std::string traj_graph_key(const bann_ctx* ctx, const Plan& p, int32_t L)
   put((int64_t)(intptr_t)p.d_gx);
   put((int64_t)(intptr_t)p.d_gxpre);
   for (const auto& g : p.groups) {
-    put(g.kind), put(g.L), put(g.act), put(g.nw), put(g.full);
+    put(g.kind), put(g.L), put(g.act), put(g.nw), put(g.cpw), put(g.full);  // cpw: fxl's template and LDS size
     put((int64_t)g.items.size());
     put((int64_t)(intptr_t)g.d_items);
   }
@@ -2036,7 +2037,12 @@ extern "C" int bann_leapfrog_steps(bann_ctx* ctx, int32_t k) {
   if (k < 0 || ctx->lf_step + k > ctx->lf_L) return fail(ctx, BANN_E_ARG, "steps beyond the trajectory length");
   for (int i = 0; i < k; ++i) {
     const int step = ++ctx->lf_step;
-    tm_mark_follow(ctx, TM_GRAD0);  // the previous step's (or the session start's) end
+    // the previous step's end -- within this call only: between calls the caller may
+    // have enqueued work of its own, so a call's first step records a fresh mark
+    if (i == 0)
+      tm_mark(ctx, TM_GRAD0);
+    else
+      tm_mark_follow(ctx, TM_GRAD0);
     int rc = grad_update(ctx, ctx->lf, step == ctx->lf_L ? 1 : 0, step < ctx->lf_L ? MODE_STEP : MODE_LAST, step);
     if (rc) return rc;
     tm_mark(ctx, TM_UPD1);

@@ -302,6 +302,25 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   if (status != BANN_ACCEPTED) {  // every local branch back to theta_0, predictions to f(theta_0)
     run_update(ctx, p, MODE_RESTORE, 0);
     launch_restore_pred(ctx->st, p.d_all, nb, ctx->stream);
+    // e at theta_0 (the step-L error of the netsum buffer belongs to theta_L): the
+    // restored outputs summed over branches and ranks, no genotype pass
+    launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
+    rc = allreduce_device_f32(ctx, ctx->d_netsum, n);
+    if (rc) return rc;
+    launch_net_targets(ctx->st, p.d_all, 0, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart, ctx->d_netrss + L,
+                       ctx->stream);
+  }
+  // the final state's Gibbs targets and residual: y_b = f_b - e = y - bias - sum_{c != b} f_c
+  // for every local branch (net.rs:279-280) and the context's device residual
+  // y - bias - sum_b f_b = -e, so a branch sampler or bann_rebuild_targets that follows sees
+  // the network where this trajectory left it
+  launch_net_targets(ctx->st, p.d_all, nb, ctx->d_netsum, nullptr, 0.f, nullptr, nullptr, ctx->stream);
+  {
+    float* res = nullptr;
+    rc = bann_residual_device(ctx, &res);
+    if (rc) return rc;
+    CK(hipMemsetAsync(res, 0, n * sizeof(float), ctx->stream));
+    launch_residual_sub(res, ctx->d_netsum, n, ctx->stream);
   }
   mark_predictions(ctx, p, true);
   CK(hipGetLastError());

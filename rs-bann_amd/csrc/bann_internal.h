@@ -187,7 +187,8 @@ void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, i
 // scratch: residual_delta_scratch_floats(n)
 void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, float* out, float* scratch,
                     hipStream_t s);
-// sum_e: in = sum over ranks of the branch outputs, out = the error e; part: net_scratch_doubles(n)
+// sum_e: in = sum over ranks of the branch outputs, out = the error e; part: net_scratch_doubles(n);
+// y = null: sum_e already holds e and only the nb branch targets y_b = f_b - e are written
 void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
                         float bias, double* part, double* rss_out, hipStream_t s);
 int64_t net_scratch_doubles(int64_t n);

@@ -1013,17 +1013,15 @@ int train_record(bann_net* t, int chain_ix, const bann_mcmc_cfg* cfg, const std:
 namespace {
 // the driver's one-branch trajectories are launch-latency-bound: replay each as one
 // captured HIP graph (bann_set_graph_replay) unless BANN_HMC_GRAPH=0; the
-// context's own setting (BANN_HMC_GRAPH=1, default off) is restored after training
+// context's previous setting is restored after training
 struct GraphReplayScope {
   bann_ctx* ctx;
-  explicit GraphReplayScope(bann_ctx* c) : ctx(c) {
+  int32_t prev;
+  explicit GraphReplayScope(bann_ctx* c) : ctx(c), prev(bann_get_graph_replay(c)) {
     const char* e = std::getenv("BANN_HMC_GRAPH");
     (void)bann_set_graph_replay(ctx, !e || std::atoi(e) != 0);
   }
-  ~GraphReplayScope() {
-    const char* e = std::getenv("BANN_HMC_GRAPH");
-    (void)bann_set_graph_replay(ctx, e && std::atoi(e) != 0);
-  }
+  ~GraphReplayScope() { (void)bann_set_graph_replay(ctx, prev); }
 };
 }  // namespace
 

@@ -580,7 +580,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     __syncthreads();
     const int narr = folds ? folds[it.fold_ix].nslab : bd.nsplits;
     if (threadIdx.x == 0)
-      s_last = !pub || __hip_atomic_fetch_add(&upd_cnt[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == narr - 1;
+      s_last = !pub || __hip_atomic_fetch_add(&upd_cnt[b], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == narr - 1;
     __syncthreads();
     if (s_last) {
       if (pub) {

@@ -507,8 +507,10 @@ int64_t net_scratch_doubles(int64_t n) { return (n + NET_BLK - 1) / NET_BLK; }
 void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
                         float bias, double* part, double* rss_out, hipStream_t s) {
   const int nparts = (int)((st.n + NET_BLK - 1) / NET_BLK);
-  hipLaunchKernelGGL(k_net_err, dim3(nparts), dim3(NET_BLK), 0, s, st.n, sum_e, y, bias, part);
-  hipLaunchKernelGGL(k_net_rss, dim3(1), dim3(64), 0, s, part, nparts, rss_out);
+  if (y) {  // y = null: sum_e already holds e, only the targets are written
+    hipLaunchKernelGGL(k_net_err, dim3(nparts), dim3(NET_BLK), 0, s, st.n, sum_e, y, bias, part);
+    hipLaunchKernelGGL(k_net_rss, dim3(1), dim3(64), 0, s, part, nparts, rss_out);
+  }
   if (nb > 0)
     hipLaunchKernelGGL(k_net_targets, dim3((unsigned)((st.n + 255) / 256), (unsigned)nb), dim3(256), 0, s, st,
                        branches, sum_e);

@@ -923,10 +923,12 @@ def test_graph_replay_matches_launches(Ctx):
     """bann_set_graph_replay: a trajectory replayed as one captured HIP graph
     gives the bits of the launch-by-launch trajectory -- status, -H trace,
     parameters and prediction rows -- over several branch sets and L (graphs are
-    keyed by plan shape, L and the kernels' by-value state)."""
+    keyed by plan shape, L and the kernels' by-value state; fxl branches of 4 and
+    8 marker chunks per wave -- different templates and LDS sizes -- included)."""
     rng = np.random.default_rng(41)
     n = 900
-    shapes = [(60, [4, 4, 1]), (120, [4, 3, 1]), (40, [8, 8, 1]), (30, [6, 5, 3, 1])]
+    shapes = [(60, [4, 4, 1]), (120, [4, 3, 1]), (40, [8, 8, 1]), (30, [6, 5, 3, 1]), (1300, [4, 4, 1]),
+              (2200, [4, 4, 1])]
     g = O.synthetic_genotypes(rng, n, sum(m for m, _ in shapes))
     specs, off = [], 0
     for m, w in shapes:
@@ -936,7 +938,9 @@ def test_graph_replay_matches_launches(Ctx):
         off += m
     ctxs = [build_context(Ctx, g, specs) for _ in range(2)]
     ctxs[1].set_graph_replay(True)
-    for it, (bl, L) in enumerate([([0], 3), ([0, 1], 5), ([2], 4), ([0], 3), ([3, 1], 6), ([0, 1], 5)]):
+    assert ctxs[0].kernel_path(4) == ctxs[0].kernel_path(5) == "fused_large"
+    for it, (bl, L) in enumerate([([0], 3), ([0, 1], 5), ([2], 4), ([0], 3), ([3, 1], 6), ([0, 1], 5), ([4], 3),
+                                  ([5], 3), ([4, 5], 4), ([4], 3), ([5], 3)]):
         out = [c.hmc_step(bl, L, 10.0, step_factor=0.3, seed=100 + it) for c in ctxs]
         assert np.array_equal(out[0]["status"], out[1]["status"]), it
         assert np.array_equal(out[0]["trace"], out[1]["trace"], equal_nan=True), it

@@ -58,6 +58,17 @@ def _draws(rng, specs, L):
     return eps, mom
 
 
+def _check_final_targets(ctx, brs, Xs, y, bias):
+    """the state bann_network_hmc_step leaves (include/bann.h): the device residual is
+    y - bias - sum_b f_b of the final parameters (accepted or restored) and every
+    branch's target is its Gibbs target f_b - e, so rss against it is the network's"""
+    r = y - bias - sum(O.predict(br, X) for br, X in zip(brs, Xs))
+    assert norm_rel(ctx.residual_get(), r) < 1e-5
+    rss = float(np.sum(r * r))
+    for b in range(len(brs)):
+        assert abs(ctx.rss(b) - rss) <= 1e-5 * rss, (b, ctx.rss(b), rss)
+
+
 def test_network_hmc_matches_oracle():
     rng, g, specs = _problem()
     n, L = g.shape[1], 6
@@ -79,6 +90,7 @@ def test_network_hmc_matches_oracle():
         assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (res["trace"], tr)
         for b, br in enumerate(brs):
             assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+        _check_final_targets(ctx, brs, Xs, y, bias)
         for s, br in zip(specs, brs):
             s["branch"] = f32_branch(br)
             s["branch"].error_precision = specs[0]["branch"].error_precision
@@ -283,6 +295,7 @@ def test_network_hmc_fx_only_matches_oracle(monkeypatch, net_err, big):
         assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (res["trace"], tr)
         for b, br in enumerate(brs):
             assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+        _check_final_targets(ctx, brs, Xs, y, 0.1)
         for s, br in zip(specs, brs):
             s["branch"] = f32_branch(br)
     ctx.close()
