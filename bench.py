@@ -133,6 +133,11 @@ def cpu_baseline(n, m, widths, sample_branches, sample_steps):
     return dict(branch_steps_per_s=branch_steps_per_s, threads=threads, seconds=t, setup_s=setup.value)
 
 
+def _fin(x):
+    """a float for the JSON line, None where it is not finite (json has no infinity)"""
+    return float(x) if math.isfinite(x) else None
+
+
 def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net, args, nb, L=20):
     """one network-joint trajectory (bann_network_hmc_step) through the library's
     communicator, timed per phase with HIP events: RCCL's own rank count
@@ -163,7 +168,11 @@ def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net
         dist.all_reduce(tr, op=dist.ReduceOp.MIN)
         ranks_seen = [float(tr[0])]
     el, ar_ms, fwd_ms, grad_ms, upd_ms = vals
-    return {"n_gpus": world, "comm": info["kind"] if info["kind"] == "rccl" else f"callback ({backend})",
+    rule = ctx.network_step_rule_info()
+    return {"step_rule": {"kind": args.network_step_rule, "tau": args.network_tau,
+                          "fraction_scaled": rule["fraction_scaled"], "mode_before": _fin(rule["mode_before"]),
+                          "mode_after": _fin(rule["mode_after"])},
+            "n_gpus": world, "comm": info["kind"] if info["kind"] == "rccl" else f"callback ({backend})",
             "comm_ranks_reported": int(ranks_seen[0]), "L": L, "step_factor": factor,
             "status": {0: "accepted", 1: "rejected", 2: "rejected_early"}[r["status"]],
             "steps_per_s": L / el, "allreduces": n_ar, "allreduce_us_per_step": 1e3 * ar_ms,
@@ -248,6 +257,11 @@ def main():
                     help="skip the untimed network-joint trajectory through the library's RCCL communicator "
                          "(a 1-rank one at N = 1) that runs before the warmup and is reported in the line "
                          "(network_check)")
+    ap.add_argument("--network-step-rule", default="common_mode", choices=["common_mode", "off"],
+                    help="network-joint step sizes: the common-mode water-filling rule (bann_set_network_step_rule, "
+                         "default) or the per-branch Izmailov steps as they are")
+    ap.add_argument("--network-tau", type=float, default=1.0,
+                    help="common-mode rule: omega eps of the network's common mode after the rule")
     ap.add_argument("--accept-trajectories", type=int, default=None,
                     help="untimed trajectories after the timed one whose acceptance is reported beside it "
                          "(default 4 for --sampler network: one Metropolis decision per trajectory)")
@@ -299,6 +313,7 @@ def main():
     for k in range(nb):
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
+    ctx.set_network_step_rule(args.network_step_rule == "common_mode", args.network_tau)
     path = ctx.kernel_path(0)
     assert path == ("layered" if heavy else "wide" if widths[0] > 4 else "fused" if m_b <= 512 else "fused_large")
     assert all(ctx.kernel_path(k) == path for k in range(nb))
@@ -616,6 +631,12 @@ def main():
             "sampler": args.sampler,
             "setup_s": setup_s,
         }
+        if args.sampler == "network":
+            rule = ctx.network_step_rule_info()
+            out["network_step_rule"] = {"kind": args.network_step_rule, "tau": args.network_tau,
+                                        "fraction_scaled": rule["fraction_scaled"],
+                                        "mode_before": _fin(rule["mode_before"]),
+                                        "mode_after": _fin(rule["mode_after"])}
         if netcheck is not None:
             out["network_check"] = netcheck
         if args.emulate_shard:

@@ -402,6 +402,22 @@ int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambd
                           float max_hamiltonian_error, int32_t step_mode, float step_factor, const float* eps,
                           const float* momentum, uint64_t seed, const float* u, int32_t* status_out,
                           double* h_trace_out, double* rss_out);
+/* Step sizes of the network-joint state (no reference counterpart: the network
+ * sampler is this library's).  With per-branch Izmailov / uniform
+ * steps the joint leapfrog's stiffest direction is the common mode -- every branch
+ * shifting the network output together -- whose curvature grows with the number
+ * of branches B (B aligned branches: B times one branch's).  common_mode = 1
+ * (default, tau = 1): before each trajectory one extra gradient launch with output
+ * error 1 gives g = J^T 1 (the gradient of sum_i F_i) and every step size becomes
+ * eps_p min(1, t / (eps_p |g_p|)) with the largest t (within 2^(1/4)) such that
+ * lambda_e / n sum_p min(eps_p |g_p|, t)^2 <= tau^2: the common mode runs at
+ * omega eps <= tau while the parameters that do not drive it keep their steps.
+ * Summed over the ranks (collective); not applied to injected step sizes. */
+int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau);
+/* the last network trajectory's rule: [threshold t (inf: no step changed),
+ * (omega eps)^2 of the common mode before (inf when some single parameter alone
+ * exceeded tau) and after, the fraction of parameters whose step was reduced] */
+int bann_network_step_rule_info(const bann_ctx* ctx, double* out4);
 
 /* ---------------- introspection for tests / profiling ---------------- */
 /* which gradient kernel serves branch b: 1 = fx fused single-pass kernel (every

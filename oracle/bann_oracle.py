@@ -785,6 +785,42 @@ def network_hmc_step(brs: Sequence[Branch], Xs, y, bias: float, lambda_e: float,
     return dict(status=status, trace=trace, rss=r)
 
 
+def common_mode_gains(brs: Sequence[Branch], Xs):
+    """g_b = J_b^T 1 per branch (param_vec order): the gradient of sum_i f_b(i), i.e. the
+    half-rss backward (branch_sampler.rs:813-875) against the target f_b - 1."""
+    gs = []
+    for b, X in zip(brs, Xs):
+        f = predict(b, X)
+        _, dW, db = backpropagate(b, X, f - 1.0)
+        gs.append(param_vec(dW, db))
+    return gs
+
+
+def common_mode_steps(brs: Sequence[Branch], Xs, eps_list, lambda_e: float, tau: float = 1.0):
+    """The network-joint step-size rule (bann_set_network_step_rule; no reference counterpart,
+    DESIGN.md 7), exact water-filling in f64: with a_p = eps_p |g_p| (g = J^T 1 over every
+    branch), eps_p min(1, t / a_p) with the largest t such that lambda_e / n sum_p min(a_p, t)^2
+    <= tau^2 (t = inf when the unscaled sum already is).  Returns (new eps list, t, a list)."""
+    n = Xs[0].shape[0]
+    gs = common_mode_gains(brs, Xs)
+    a = [np.asarray(e, np.float64) * np.abs(g) for e, g in zip(eps_list, gs)]
+    allv = np.sort(np.concatenate(a))[::-1]
+    T = tau * tau * n / lambda_e
+    if float(np.sum(allv * allv)) <= T:
+        return [np.asarray(e, np.float64).copy() for e in eps_list], math.inf, a
+    # f(t) = k t^2 + sum_{p >= k} a_(p)^2 with the k largest capped: find the crossing
+    tail = np.concatenate([np.cumsum((allv * allv)[::-1])[::-1], [0.0]])
+    t = 0.0
+    for k in range(1, allv.size + 1):
+        # t in [a_(k), a_(k-1)] with k capped: k t^2 + tail[k] = T
+        tk2 = (T - tail[k]) / k
+        lo = allv[k] if k < allv.size else 0.0
+        if tk2 >= lo * lo:
+            t = math.sqrt(max(tk2, 0.0))
+            break
+    return [np.asarray(e, np.float64) * np.minimum(1.0, t / np.maximum(x, 1e-300)) for e, x in zip(eps_list, a)], t, a
+
+
 # --------------------------------------------------------------------------
 # Gibbs precision posteriors (host side): gibbs_steps.rs, ridge_ard.rs:271-301
 # --------------------------------------------------------------------------

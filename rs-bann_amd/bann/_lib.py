@@ -132,6 +132,8 @@ SIGNATURES = {
     "bann_network_hmc_step": (C.c_int, [_P, _pf32, _f32, _f32, _i32, _f32, _i32, _f32, _pf32, _pf32, _u64, _pf32,
                                         _pi32, _pf64, _pf64]),
     "bann_exchange_residual_device": (C.c_int, [_P]),
+    "bann_set_network_step_rule": (C.c_int, [_P, _i32, _f32]),
+    "bann_network_step_rule_info": (C.c_int, [_P, _pf64]),
     "bann_residual_set": (C.c_int, [_P, _pf32]),
     "bann_residual_get": (C.c_int, [_P, _pf32]),
     "bann_residual_device": (C.c_int, [_P, C.POINTER(_pf32)]),

@@ -436,6 +436,18 @@ class BannContext:
             C.byref(rss)))
         return dict(status=st.value, trace=tr, rss=rss.value)
 
+    def set_network_step_rule(self, common_mode: bool = True, tau: float = 1.0):
+        """the network-joint state's step sizes (bann_set_network_step_rule): the common-mode
+        water-filling rule at omega eps <= tau (default on), or the per-branch steps as given."""
+        self._check(self._lib.bann_set_network_step_rule(self._h, int(common_mode), float(tau)))
+
+    def network_step_rule_info(self) -> dict:
+        """the last network trajectory's rule: threshold t, (omega eps)^2 of the common mode
+        before and after, the fraction of parameters whose step was reduced."""
+        out = np.zeros(4, np.float64)
+        self._check(self._lib.bann_network_step_rule_info(self._h, _ptr(out, C.c_double)))
+        return dict(threshold=out[0], mode_before=out[1], mode_after=out[2], fraction_scaled=out[3])
+
     def exchange_residual_device(self):
         """device residual -= sum over ranks of the last session's residual change (collective)."""
         self._check(self._lib.bann_exchange_residual_device(self._h))

@@ -185,6 +185,91 @@ extern "C" int bann_exchange_residual_device(bann_ctx* ctx) {
   return BANN_OK;
 }
 
+extern "C" int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau) {
+  if (!ctx) return BANN_E_ARG;
+  if (common_mode && !(tau > 0.f)) return fail(ctx, BANN_E_ARG, "tau must be positive");
+  ctx->cm_rule = common_mode != 0;
+  ctx->cm_tau = tau;
+  return BANN_OK;
+}
+
+extern "C" int bann_network_step_rule_info(const bann_ctx* ctx, double* out4) {
+  if (!ctx || !out4) return BANN_E_ARG;
+  for (int k = 0; k < 4; ++k) out4[k] = ctx->cm_info[k];
+  return BANN_OK;
+}
+
+namespace {
+// the common-mode rule (bann.h bann_set_network_step_rule; kernels_update.hip k_cm_*): one gradient
+// launch with output error 1 gives g = J^T 1 of every local branch, the histogram of
+// r_p = (eps_p g_p)^2 / T is summed over branches and ranks, and eps_p *= min(1, t / (eps_p |g_p|))
+// with the largest candidate t^2 = T 2^(-k/2) whose sum_p min(eps_p |g_p|, t)^2 <= T = tau^2 n / lambda_e
+int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e) {
+  const int64_t n = ctx->n;
+  const int32_t nb = (int32_t)p.all.size();
+  if (!ctx->d_ones) {
+    CK(dalloc(&ctx->d_ones, n));
+    std::vector<float> one((size_t)n, 1.f);
+    CK(hipMemcpy(ctx->d_ones, one.data(), n * sizeof(float), hipMemcpyHostToDevice));
+    CK(dalloc(&ctx->d_cm, ((int64_t)ctx->br.size() + 1) * 2 * CM_NC));
+  }
+  if (!fx_only) {  // every branch's target f_b - 1 (the prediction rows at theta_0 first)
+    int rc = run_forward(ctx, p);
+    if (rc) return rc;
+    launch_net_targets(ctx->st, p.d_all, nb, ctx->d_ones, nullptr, 0.f, nullptr, nullptr, ctx->stream);
+  }
+  ctx->st.nete = fx_only ? ctx->d_ones : nullptr;
+  int rc = run_grad(ctx, p, 0);
+  ctx->st.nete = fx_only ? ctx->d_netsum : nullptr;
+  if (rc) return rc;
+  const double T = (double)ctx->cm_tau * ctx->cm_tau * (double)n / (double)lambda_e;
+  unsigned long long* d_out = ctx->d_cm + (int64_t)ctx->br.size() * 2 * CM_NC;
+  launch_cm_hist(ctx->st, p.d_all, nb, (float)(1.0 / T), ctx->d_cm, d_out, ctx->stream);
+  CK(hipGetLastError());
+  unsigned long long hist[2 * CM_NC];
+  CK(hipMemcpyAsync(hist, d_out, sizeof(hist), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  std::vector<double> h(2 * CM_NC);
+  for (int k = 0; k < 2 * CM_NC; ++k) h[k] = (double)hist[k];
+  rc = allreduce_host_f64(ctx, h.data(), 2 * CM_NC);  // over ranks: every rank picks the same t
+  if (rc) return rc;
+  // f_k / T = 2^(-k/2) #{r >= 2^(-k/2)} + sum_{r < 2^(-k/2)} r, in bins (bin j >= 1 holds
+  // 2^(-j/2) <= r < 2^(-(j-1)/2); its r sum in units of 2^-38)
+  std::vector<double> tail(CM_NC + 1, 0.0);  // tail[k] = sum of r over bins > k
+  for (int k = CM_NC - 1; k >= 1; --k) tail[k - 1] = tail[k] + h[CM_NC + k] * 0x1p-38;
+  double total = 0.0;
+  for (int k = 0; k < CM_NC; ++k) total += h[k];
+  double cnt = 0.0;
+  int kst = -1;
+  if (h[0] > 0.0 || tail[0] > 1.0) {
+    kst = CM_NC - 1;
+    for (int k = 0; k < CM_NC; ++k) {
+      cnt += h[k];
+      if (k >= 1 && std::pow(2.0, -0.5 * k) * cnt + tail[k] <= 1.0) {
+        kst = k;
+        break;
+      }
+    }
+  }
+  if (kst < 0) {  // the common mode is already below tau: steps unchanged
+    ctx->cm_info[0] = INFINITY;
+    ctx->cm_info[1] = ctx->cm_info[2] = tail[0] * ctx->cm_tau * ctx->cm_tau;
+    ctx->cm_info[3] = 0.0;
+    return BANN_OK;
+  }
+  double scaled = 0.0;
+  for (int k = 0; k <= kst; ++k) scaled += h[k];
+  const double t = std::sqrt(T * std::pow(2.0, -0.5 * kst));
+  launch_cm_apply(ctx->st, p.d_all, nb, p.max_p, (float)t, ctx->stream);
+  CK(hipGetLastError());
+  ctx->cm_info[0] = t;
+  ctx->cm_info[1] = h[0] > 0.0 ? INFINITY : tail[0] * ctx->cm_tau * ctx->cm_tau;  // (omega eps)^2 of the mode
+  ctx->cm_info[2] = (std::pow(2.0, -0.5 * kst) * scaled + tail[kst]) * ctx->cm_tau * ctx->cm_tau;
+  ctx->cm_info[3] = total > 0.0 ? scaled / total : 0.0;
+  return BANN_OK;
+}
+}  // namespace
+
 extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambda_e, int32_t L,
                                      float max_dh, int32_t step_mode, float factor, const float* eps,
                                      const float* momentum, uint64_t seed, const float* u, int32_t* status_out,
@@ -245,6 +330,14 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
     tm_mark(ctx, TM_GRAD1);
     return r;
   };
+  if (ctx->cm_rule && step_mode != BANN_STEP_INJECTED && lambda_e > 0.f) {
+    rc = common_mode_steps(ctx, p, fx_only, lambda_e);
+    if (rc) {
+      ctx->st.netmode = 0;
+      ctx->st.nete = nullptr;
+      return rc;
+    }
+  }
   rc = forward_and_targets(0);
   if (!rc) {
     launch_snapshot_pred(ctx->st, p.d_all, nb, ctx->stream);

@@ -192,6 +192,14 @@ void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, flo
 void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,
                         float bias, double* part, double* rss_out, hipStream_t s);
 int64_t net_scratch_doubles(int64_t n);
+// common-mode step sizes of the network-joint state (kernels_update.hip): per branch the common-mode
+// gains a_p = eps_p |g_p| (g: the branch's partial slabs after a gradient launch with output error 1)
+// into st.grad and a histogram of a_p^2 / T (part: nb x 2 CM_NC, out: 2 CM_NC = counts, then
+// fixed-point sums in units of 2^-38); then eps_p *= min(1, t / a_p)
+#define CM_NC 96
+void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, float inv_T, unsigned long long* part,
+                    unsigned long long* out, hipStream_t s);
+void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, hipStream_t s);
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
 // mode 0 exact f32 MFMA, 1 bf16 MFMA, 2 f32-accurate bf16 planes (kernels_wx.hip)
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int mode,

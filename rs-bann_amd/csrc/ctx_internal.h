@@ -139,6 +139,12 @@ struct bann_ctx {
   double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)
   double* d_netpart = nullptr; // network mode: rss block partials
   int32_t netrss_cap = 0;
+  // network mode: the common-mode step-size rule (bann_set_network_step_rule)
+  int32_t cm_rule = 1;
+  float cm_tau = 1.0f;
+  float* d_ones = nullptr;                 // n ones: the output error of the common-mode gradient launch
+  unsigned long long* d_cm = nullptr;      // per-branch histograms (nbranch x 2 CM_NC), then their sum
+  double cm_info[4] = {0.0, 0.0, 0.0, 0.0};  // last trajectory: threshold t, bound before / after (omega eps)^2, scaled fraction
   double* d_ar64 = nullptr;    // RCCL all-reduce of host f64 vectors (the network -H trace): reused device buffer
   int64_t ar64_cap = 0;
   // the network residual on the device (bann_residual.hip): n floats, reduction scratch, pinned (sum, sum sq)

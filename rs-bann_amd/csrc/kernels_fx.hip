@@ -48,6 +48,37 @@
 #define FX_WAVES 4        // waves per workgroup (one work item, tiles interleaved)
 #define FX_SLOT 8192      // one tile image at <= 8 chunks (512 markers x 16 B)
 #define FX_DROW 256       // delta0 digit image: 16 rows x 16 B per K group (read twice per tile)
+
+// Profiling builds only (tools/build_ab.sh <tag> "-DFX_STAMPS=1" / "-DFX_ABL=<bits>"); both 0 in the
+// product, where they generate no code.  FX_STAMPS: per-phase shader-cycle sums of k_fused_grad_fx
+// (s_memtime) into DevState::dbg, printed at bann_ctx_destroy under BANN_STAMPS=1: p0 wait for the
+// tile, p1 forward, p2 head, p3 delta0 digits, p4 backward, p5 loop overhead, p6 realtime (100 MHz),
+// p7 loop cycles.  FX_ABL (results wrong, timing only): 1 forward without the 2-bit unpack, 2 backward
+// without it, 4 no head (delta0 = z0), 8 no MFMAs (the operands XORed into the accumulators), 16 no
+// genotype / target stream (the loop computes on whatever the slots hold).
+#ifndef FX_STAMPS
+#define FX_STAMPS 0
+#endif
+#ifndef FX_ABL
+#define FX_ABL 0
+#endif
+#if FX_STAMPS
+#define FX_STAMP(i)                                            \
+  do {                                                         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_last;                                      \
+    t_last = t_;                                               \
+  } while (0)
+#else
+#define FX_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+#if FX_ABL & 8
+#define FX_MFMA(a, b, c) ((c) + ((a) ^ (b)))
+#else
+#define FX_MFMA(a, b, c) __builtin_amdgcn_mfma_i32_16x16x64_i8((a), (b), (c), 0, 0, 0)
+#endif
 // The stream runs TWO tiles ahead in the same two slots: chunk c of tile t + 2
 // is issued into tile t's slot as soon as tile t's backward has read chunk c's
 // last window (the target piece once the head has read the target), so a piece
@@ -121,6 +152,16 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
                                                   false, false);
   a = __builtin_bit_cast(float, (unsigned)r[0]);
   b = __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+#ifndef FX_FWDPIPE
+#define FX_FWDPIPE 0
+#endif
+// forward fragment q of a 16-marker quad-byte operand: field q of every byte, in place
+// (x 4^q, folded into the digit combine) except q = 3 (bits 6-7 would overflow int8)
+__device__ __forceinline__ v4i fx_field(v4u x, int q) {
+  return q == 0 ? (v4i)(x & 0x03030303u)
+                : q == 1 ? (v4i)(x & 0x0C0C0C0Cu) : q == 2 ? (v4i)(x & 0x30303030u) : (v4i)((x >> 2u) & 0x30303030u);
 }
 
 // NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
@@ -211,6 +252,12 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   float* predb = st.pred + bd.y_off;
   const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
+#if FX_ABL & 128
+  const uint64_t xb = (uint64_t)(uintptr_t)(reinterpret_cast<const char*>(st.xu2) + bd.x_off);
+  const char* xbase_s = reinterpret_cast<const char*>(
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xb >> 32)) << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xb));
+#endif
 
   // LDS-DMA of the NEXT tile is spread over the current tile's forward phase
   // (one 1 KiB piece per chunk, the target piece in the head): issued in one
@@ -222,10 +269,17 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   // (Row 0 is never padding, so the wave's instruction -- one vmcnt count -- always issues.)
   const bool pad_row = 64 * (nch - 1) + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
   auto issue_chunk = [&](int tt, int sl, int c) {
+    if (FX_ABL & 16) return;
     if (c == nch - 1 && pad_row) return;
+#if FX_ABL & 128
+    glds16_s(xbase_s + (uint64_t)tt * (uint64_t)tile_bytes + (uint64_t)(c * 1024), (uint32_t)lane * 16u,
+             &s_x[wave][sl][c * 1024]);
+#else
     glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
+#endif
   };
   auto issue_y = [&](int tt, int sl) {
+    if (FX_ABL & 16) return;
     const int64_t row = 64 * (int64_t)tt + iota;
     glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
   };
@@ -249,24 +303,31 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
   }
 
+#if FX_STAMPS
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ntl = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
+  unsigned long long t_last = mt0;
+#endif
   int tt = tb + wave, sl = 0;
   if (tt < te) {
     for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
-    if (tt + NW < te) {
+    if (tt + NW < te && !(FX_ABL & 64)) {
       for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
       issue_y(tt + NW, 1);
     }
   }
   for (; tt < te; tt += NW, sl ^= 1) {
-    const bool more = tt + NW < te;
-    const bool more2 = tt + 2 * NW < te;  // tile tt + 2 NW goes into this slot
+    const bool more = tt + NW < te && !(FX_ABL & 64);
+    const bool more2 = tt + 2 * NW < te && !(FX_ABL & 64);  // tile tt + 2 NW goes into this slot
     // tile tt (issued during tile tt - NW) has landed.  (An L2 prefetch of the
     // tile after it measured +3 %: with 8 waves/CU the L2 is already the DMA's
     // working set.)
     // the nch + 1 pieces of tile tt + NW are younger (loads return in order; a
     // younger pred store still outstanding only makes this wait longer)
+    FX_STAMP(5);
     vm_wait(more ? nch + 1 : 0);
+    FX_STAMP(0);
     const char* xs = &s_x[wave][sl][0];
 
     // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
@@ -289,6 +350,40 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
         }
       }
+#if FX_FWDPIPE
+      // chunk c + 1's unpack is interleaved with chunk c's MFMAs (one chunk ahead): an
+      // MFMA's operand was written a chunk earlier, so no MFMA waits on the VALU that
+      // produced it; each field register is rewritten right after the MFMA that read it
+      v4i Bf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Bf[q] = fx_field(Xq[0], q);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (NCH == 0 && c >= nch) continue;
+        const v4i Ac = Aq[c % FD];
+        const bool nxt = c + 1 < 8 && (NCH != 0 || c + 1 < nch);
+        const v4u Xn = Xq[(c + 1) % FD];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, Bf[q], facc[q], 0, 0, 0);
+          if (nxt) Bf[q] = fx_field(Xn, q);
+        }
+        // each MFMA, then the next chunk's field it frees (4 VALU; field 3: 8)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {  // chunk c's registers are free: chunk c + 2
+          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
+          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#else
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         if (NCH == 0 && c >= nch) continue;
@@ -300,24 +395,46 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         }
         // fragment q = field q of every byte, kept in place (x 4^q, folded into the
         // digit combine below) except q = 3 (bits 6-7 would overflow int8)
+#if FX_ABL & 1
+        const v4i B0 = (v4i)Xc, B1 = (v4i)Xc, B2 = (v4i)Xc, B3 = (v4i)Xc;
+#elif FX_ABL & 32
+        const v4i B0 = (v4i)(Xc & 0x03030303u);
+        const v4i B1 = (v4i)(Xc & 0x0F0F0F0Fu);
+        const v4i B2 = (v4i)(Xc & 0x3F3F3F3Fu);
+        const v4i B3 = (v4i)Xc;
+#else
         const v4i B0 = (v4i)(Xc & 0x03030303u);
         const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
         const v4i B2 = (v4i)(Xc & 0x30303030u);
         const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
-        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B0, facc[0], 0, 0, 0);
-        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B1, facc[1], 0, 0, 0);
-        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B2, facc[2], 0, 0, 0);
-        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
+#endif
+        facc[0] = FX_MFMA(Ac, B0, facc[0]);
+        facc[1] = FX_MFMA(Ac, B1, facc[1]);
+        facc[2] = FX_MFMA(Ac, B2, facc[2]);
+        facc[3] = FX_MFMA(Ac, B3, facc[3]);
         __builtin_amdgcn_sched_barrier(0);
       }
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(1);
+#if FX_ABL & 64
+    if (tt + NW < te) {  // one tile ahead, issued in the VALU-only head phase
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, sl ^ 1, c);
+      issue_y(tt + NW, sl ^ 1);
+    }
+#endif
     // the head + digit phase is a dependent VALU chain: at raised priority it
     // takes the SIMD's issue slots ahead of the partner wave's independent
     // MFMA/unpack stream (measured -1 %)
     __builtin_amdgcn_s_setprio(1);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
+#if FX_ABL & 32
+    facc[3] = (facc[3] - facc[2]) >> 6;
+    facc[2] = (facc[2] - facc[1]) >> 4;
+    facc[1] = (facc[1] - facc[0]) >> 2;
+#endif
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
     float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
     swap32(z0, z2);
@@ -330,6 +447,11 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     const bool valid = row < n;
     const float yv = s_y[wave][sl][lane];
     float d[4];
+#if FX_ABL & 4
+    d[0] = z0 + yv, d[1] = z1, d[2] = z2, d[3] = z3;
+    if (write_pred && valid) predb[row] = z0;
+    rss += (double)z1;
+#else
     {
       const auto& Wh = uW;
       const auto& Bh = uB;
@@ -388,12 +510,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         }
       }
     }
+#endif
 
     if (more2) {  // the target has been read (yv in a register): its slot takes tile tt + 2 NW's
       asm volatile("" ::"v"(yv));
       issue_y(tt + 2 * NW, sl);
     }
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(2);
     // the backward's first genotype windows: their LDS reads fly under the digit phase
     constexpr int PD = 8;
     uint32_t wq[PD];
@@ -444,14 +568,19 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     *reinterpret_cast<v4u*>(sd_w) = w;
 
     __builtin_amdgcn_sched_barrier(0);
+    FX_STAMP(3);
     __builtin_amdgcn_s_setprio(0);
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     {
       // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
       auto unpack = [](uint32_t wv) -> v4i {
+#if FX_ABL & 2
+        return v4i{(int)wv, (int)wv, (int)wv, (int)wv};
+#else
         return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
                    (int)((wv >> 6) & 0x03030303u)};
+#endif
       };
       // window u + 2 is unpacked beside window u's MFMA: the MFMA's B operand was
       // written two iterations earlier, so no VALU -> MFMA hazard padding per window
@@ -468,12 +597,24 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         }
         if (u + PD < 32 && (NCH != 0 || u + PD < 4 * nch))  // slot of window u, consumed two iterations ago
           wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
-        acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
+        acc[u] = FX_MFMA(A, Bv, acc[u]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    FX_STAMP(4);
+#if FX_STAMPS
+    ++ntl;
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if FX_STAMPS
+  ph[6] = __builtin_amdgcn_s_memrealtime() - rt0;
+  ph[7] = __builtin_amdgcn_s_memtime() - mt0;
+  if (lane == 0 && st.dbg) {
+    for (int i = 0; i < 8; ++i) atomicAdd(&st.dbg[i], ph[i]);
+    atomicAdd(&st.dbg[15], ntl);
+  }
+#endif
 
   // ---- workgroup reduction (fixed order: deterministic) ----
   {
@@ -762,6 +903,40 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
           Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
         }
       }
+#if FX_FWDPIPE
+      // chunk c + 1's unpack is interleaved with chunk c's MFMAs (one chunk ahead): an
+      // MFMA's operand was written a chunk earlier, so no MFMA waits on the VALU that
+      // produced it; each field register is rewritten right after the MFMA that read it
+      v4i Bf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Bf[q] = fx_field(Xq[0], q);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        if (NCH == 0 && c >= nch) continue;
+        const v4i Ac = Aq[c % FD];
+        const bool nxt = c + 1 < 8 && (NCH != 0 || c + 1 < nch);
+        const v4u Xn = Xq[(c + 1) % FD];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, Bf[q], facc[q], 0, 0, 0);
+          if (nxt) Bf[q] = fx_field(Xn, q);
+        }
+        // each MFMA, then the next chunk's field it frees (4 VALU; field 3: 8)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {  // chunk c's registers are free: chunk c + 2
+          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
+          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#else
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         if (NCH == 0 && c >= nch) continue;
@@ -781,6 +956,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
         facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);

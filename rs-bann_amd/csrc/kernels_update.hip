@@ -821,3 +821,77 @@ void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, i
   const int pairs = (max_q + 1) / 2;
   hipLaunchKernelGGL(k_sample_momentum_phi, dim3((pairs + 255) / 256, nb), dim3(256), 0, s, st, branches, seed);
 }
+
+// ---- common-mode step sizes of the network-joint state (bann_network_hmc_step) ----
+// With Izmailov steps eps_p the joint leapfrog's stiffest direction is the common mode: every
+// branch shifting the network output together (u = 1/sqrt(n)); its eigenvalue of E H E is
+// lambda_e ||E J^T u||^2 = lambda_e / n sum_p a_p^2 with a_p = eps_p |g_p|, g = J^T 1 (the
+// gradient of sum_i F_i, one gradient launch with output error 1) -- B times one branch's for B
+// aligned branches.  Water-filling: d_p = min(1, t / a_p) with the largest t such that
+// sum_p min(a_p, t)^2 <= T = tau^2 n / lambda_e, so the mode sits at omega eps = tau while
+// the parameters that do not drive it keep their steps.  t is chosen among candidates
+// t_k^2 = T 2^(-k/2) from a histogram of r_p = a_p^2 / T (integer counts and fixed-point sums:
+// deterministic), summed over branches and ranks.
+// bin 0: r >= 1; bin j (1 <= j < CM_NC - 1): 2^(-j/2) <= r < 2^(-(j-1)/2); last bin: smaller
+#define CM_FIX 0x1p38  // fixed-point unit of the r sums (bins >= 1: r < 1, <= 2^25 params per bin)
+__device__ __forceinline__ int cm_bin(float r) {
+  if (!(r < 1.f)) return 0;
+  if (!(r > 0.f)) return CM_NC - 1;
+  const int j = (int)floorf(-2.f * __log2f(r)) + 1;
+  return j < 1 ? 1 : (j > CM_NC - 1 ? CM_NC - 1 : j);
+}
+
+// one workgroup per branch: a_p (into st.grad, scratch before the trajectory's first update) and
+// the branch's histogram part[b][0..CM_NC) counts, part[b][CM_NC..2 CM_NC) fixed-point r sums
+__global__ void __launch_bounds__(256) k_cm_hist(DevState st, const int32_t* __restrict__ blist, float inv_T,
+                                                 unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long h[2 * CM_NC];
+  const int bi = blockIdx.x;
+  const int b = blist[bi];
+  const BranchDev bd = st.br[b];
+  const int P = bd.P;
+  for (int k = threadIdx.x; k < 2 * CM_NC; k += 256) h[k] = 0ull;
+  __syncthreads();
+  for (int i = threadIdx.x; i < P; i += 256) {
+    float g = 0.f;
+    for (int s = 0; s < bd.nsplits; ++s) g += st.part[bd.part_off + (int64_t)s * P + i];  // k_update's order
+    const float a = st.eps[bd.p_off + i] * fabsf(g);
+    st.grad[bd.p_off + i] = a;
+    const float r = a * a * inv_T;
+    const int k = cm_bin(r);
+    atomicAdd(&h[k], 1ull);
+    if (k >= 1) atomicAdd(&h[CM_NC + k], (unsigned long long)((double)r * CM_FIX));
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 2 * CM_NC; k += 256) part[(int64_t)bi * 2 * CM_NC + k] = h[k];
+}
+
+__global__ void __launch_bounds__(2 * CM_NC) k_cm_sum(const unsigned long long* __restrict__ part, int nb,
+                                                      unsigned long long* __restrict__ out) {
+  unsigned long long v = 0ull;
+  for (int b = 0; b < nb; ++b) v += part[(int64_t)b * 2 * CM_NC + threadIdx.x];
+  out[threadIdx.x] = v;
+}
+
+// eps_p *= min(1, t / a_p)
+__global__ void __launch_bounds__(256) k_cm_apply(DevState st, const int32_t* __restrict__ blist, float t) {
+  const int b = blist[blockIdx.y];
+  const BranchDev bd = st.br[b];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < bd.P; i += gridDim.x * 256) {
+    const float a = st.grad[bd.p_off + i];
+    if (a > t) st.eps[bd.p_off + i] *= t / a;
+  }
+}
+
+void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, float inv_T, unsigned long long* part,
+                    unsigned long long* out, hipStream_t s) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(k_cm_hist, dim3(nb), dim3(256), 0, s, st, branches, inv_T, part);
+  hipLaunchKernelGGL(k_cm_sum, dim3(1), dim3(2 * CM_NC), 0, s, part, nb, out);
+}
+
+void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, hipStream_t s) {
+  if (nb <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((max_p + 255) / 256, 16);
+  hipLaunchKernelGGL(k_cm_apply, dim3(gx, (unsigned)nb), dim3(256), 0, s, st, branches, t);
+}

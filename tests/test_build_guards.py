@@ -44,10 +44,13 @@ def test_counted_fxl_instantiations_do_not_spill(tmp_path):
     assert fwd and all(spills[k] == 0 for k in fwd), {k: spills[k] for k in fwd}
 
 
-def test_production_kernels_carry_no_profiling_switches():
-    """the ablation / stamp switches live in the profiling copy
-    (tools/archive/profiling/kernels_fx_ablate.hip), not in the shipped kernels"""
-    for f in os.listdir(os.path.dirname(SRC)):
-        if f.endswith((".hip", ".h", ".cpp")):
-            txt = open(os.path.join(os.path.dirname(SRC), f)).read()
-            assert "#if BANN_ABLATE" not in txt and "FX_STAMP" not in txt, f
+def test_production_build_sets_no_profiling_switches():
+    """the fx kernel's profiling switches (FX_STAMPS phase stamps, FX_ABL ablations, FX_FWDPIPE
+    experiment; tools/build_ab.sh builds variant libraries with them) default to 0 in the source
+    and the product build (Makefile, __graft_entry__.build) defines none of them"""
+    txt = open(SRC).read()
+    for sw in ("FX_STAMPS", "FX_ABL", "FX_FWDPIPE"):
+        assert f"#ifndef {sw}\n#define {sw} 0\n#endif" in txt, sw
+    mk = open(os.path.join(os.path.dirname(SRC), "Makefile")).read()
+    entry = open(os.path.join(ROOT, "__graft_entry__.py")).read()
+    assert "-DFX_" not in mk and "-DFX_" not in entry and "BANN_ABLATE" not in mk

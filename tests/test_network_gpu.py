@@ -299,3 +299,54 @@ def test_network_hmc_fx_only_matches_oracle(monkeypatch, net_err, big):
         for s, br in zip(specs, brs):
             s["branch"] = f32_branch(br)
     ctx.close()
+
+
+@pytest.mark.parametrize("fx_only", [True, False])
+def test_common_mode_step_rule(fx_only):
+    """bann_set_network_step_rule (default on): before the trajectory one gradient launch
+    with output error 1 gives g = J^T 1, and the Izmailov steps become eps_p min(1, t / a_p),
+    a_p = eps_p |g_p|, with t the largest histogram candidate (within 2^(1/4) of the exact
+    water-filling threshold of oracle.common_mode_steps) keeping lambda_e / n sum min(a, t)^2
+    <= tau^2.  The trajectory itself matches the oracle run with the device's step sizes."""
+    rng = np.random.default_rng(13)
+    n = 1500
+    shapes = ([(60, [4, 4, 1], "ridge_ard")] * 8) if fx_only else SHAPES + [(60, [4, 4, 1], "ridge_ard")] * 4
+    M = sum(m for m, _, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w, prior in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior=prior))))
+        off += m
+    ctx = _context(g, specs, range(len(specs)))
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    f = sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+    y = (f + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    L, c, le = 6, 1.0, 2.0
+    brs = [s["branch"].copy() for s in specs]
+    eps0 = [O.param_vec(*O.izmailov_step_sizes(br, c, L)) for br in brs]
+    _, t_exact, a = O.common_mode_steps(brs, Xs, eps0, le, 1.0)
+    assert np.isfinite(t_exact)
+    mom = [rng.normal(size=s["branch"].num_params).astype(np.float32) for s in specs]
+    res = ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c,
+                               momentum=np.concatenate(mom), u=0.5)
+    info = ctx.network_step_rule_info()
+    t = info["threshold"]
+    assert t_exact * 2 ** -0.25 * (1 - 1e-4) <= t <= t_exact * (1 + 1e-4), (t, t_exact)
+    assert 0.0 < info["fraction_scaled"] < 1.0 and info["mode_after"] <= 1.0 + 1e-6
+    eps_dev = [ctx.get_step_sizes(b).astype(np.float64) for b in range(len(specs))]
+    for e0, ed, x in zip(eps0, eps_dev, a):
+        assert norm_rel(ed, e0 * np.minimum(1.0, t / x)) < 1e-5
+    out = O.network_hmc_step(brs, Xs, y, 0.1, le, eps_dev, [p.astype(np.float64) for p in mom], L, 10.0, 0.5)
+    assert res["status"] == out["status"]
+    tr = np.asarray(out["trace"])
+    assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr)))
+    for b, br in enumerate(brs):
+        assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+    ctx.set_network_step_rule(False)   # off: the plain Izmailov steps
+    ctx.network_hmc_step(y, 2, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=3)
+    eps_off = [O.param_vec(*O.izmailov_step_sizes(br, c, 2)) for br in brs]
+    for b in range(len(specs)):
+        assert norm_rel(ctx.get_step_sizes(b), eps_off[b]) < 2e-7
+    ctx.close()
