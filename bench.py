@@ -69,7 +69,7 @@ def log(*a):
 # but 0.0005 at L = 10).  The rule: c(L) = c_ref min(1, L / L_ref) -- below the L
 # it was tuned at, keep the tuned step size (and shorten the trajectory); above
 # it, keep the trajectory length (smaller steps).  (c_ref, L_ref) per line,
-# tuned on MI355X (tools/gpu_accept.sh):
+# tuned on MI355X (tools/archive/gpu_accept.sh):
 TUNED_FACTORS = {
     # (config, sampler, bf16 hidden GEMM): (c_ref, L_ref)
     ("c3", "branch", False): (1.0, 20),       # cli.rs:99-100 default c = 1
@@ -400,7 +400,7 @@ def main():
         targets are NOT rebuilt between trajectories: a simultaneous (Jacobi)
         update of 1000 overlapping branches (2M parameters, n = 50k) overshoots the
         residual -- measured: ||r||^2 +70 % after one trajectory and every later
-        trajectory rejected early (tools/diag_c3.py) -- so the
+        trajectory rejected early (tools/archive/diag_c3.py) -- so the
         residual bookkeeping of a sweep belongs to the sequential driver
         (--sampler sequential, the reference's Gauss-Seidel order) and the
         network sampler.  network sampler: one HMC state over all branches of all

@@ -431,12 +431,18 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
 #if FX_ABL & 32
-    facc[3] = (facc[3] - facc[2]) >> 6;
-    facc[2] = (facc[2] - facc[1]) >> 4;
-    facc[1] = (facc[1] - facc[0]) >> 2;
-#endif
+    float z0, z1, z2, z3;
+    {  // timing variant: cumulative fields solved in the float domain
+      const float c0 = comb4(facc[0]), c1 = comb4(facc[1]), c2 = comb4(facc[2]), c3 = comb4(facc[3]);
+      z0 = zscale * c0;
+      z1 = (0.25f * zscale) * (c1 - c0);
+      z2 = (0.0625f * zscale) * (c2 - c1);
+      z3 = fmaf(0.015625f * zscale, c3 - c2, zscale);
+    }
+#else
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
     float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
+#endif
     swap32(z0, z2);
     swap32(z1, z3);
     swap16(z0, z1);
@@ -577,6 +583,9 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
       auto unpack = [](uint32_t wv) -> v4i {
 #if FX_ABL & 2
         return v4i{(int)wv, (int)wv, (int)wv, (int)wv};
+#elif FX_ABL & 512
+        return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
+                   (int)(wv & 0xC0C0C0C0u)};  // timing variant: field 3 in place (code - 1 storage)
 #else
         return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
                    (int)((wv >> 6) & 0x03030303u)};
