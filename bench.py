@@ -76,25 +76,35 @@ TUNED_FACTORS = {
     ("c2", "branch", False): (1.0, 20),
     ("small", "branch", False): (1.0, 20),
     ("c3", "sequential", False): (1.0, 20),
-    ("c3", "network", False): (0.11, 20),     # the joint state: 0.12 sits past the stiff-mode cliff
     ("c5", "branch", False): (0.1, 20),
     ("c5", "branch", True): (0.02, 20),       # bf16-rounded hidden activations: energy error
     ("c3def", "branch", False): (0.02, 10),
-    # C5's joint state (4 000 branches, 21 M parameters): 0.01 and 0.005 diverge, 0.001
-    # rejects, 0.0005 accepts (2 of 2 trajectories at L = 20, r4c / r4d)
+    # the network-joint state with the common-mode step rule (bann_set_network_step_rule,
+    # DESIGN.md 7; round 5, 10 trajectories each at L = 20): C3 0.5 accepts 0.9 (1.0: 0.2);
+    # C5 0.005 / 0.01 accept 1.0, 0.02 accepts 0.9
+    ("c3", "network", False): (0.5, 20),
+    ("c5", "network", False): (0.02, 20),
+    ("c5", "network", True): (0.01, 20),
+}
+# ... and without it (--network-step-rule off): the stiffest joint direction -- all branches
+# moving the output together -- caps the factor: C3 0.11 accepts, 0.12 diverges; C5 0.0005
+# accepts, 0.001 rejects, 0.005 / 0.01 diverge (round 4)
+TUNED_FACTORS_NO_RULE = {
+    ("c3", "network", False): (0.11, 20),
     ("c5", "network", False): (0.0005, 20),
     ("c5", "network", True): (0.0005, 20),
 }
 
 
-def default_step_factor(config, sampler, bf16, L):
+def default_step_factor(config, sampler, bf16, L, rule="common_mode"):
     key = (config, sampler, bf16)
-    if key not in TUNED_FACTORS:   # untuned line: the branch sampler's, scaled down for the joint state
+    table = TUNED_FACTORS_NO_RULE if (sampler == "network" and rule == "off") else TUNED_FACTORS
+    if key not in table:   # untuned line: the branch sampler's, scaled down for the joint state
         c, l_ref = TUNED_FACTORS.get((config, "branch", bf16), (1.0, 20))
         if sampler == "network":
             c *= 0.1
     else:
-        c, l_ref = TUNED_FACTORS[key]
+        c, l_ref = table[key]
     return c * min(1.0, L / l_ref)
 
 
@@ -146,7 +156,7 @@ def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net
     if ctx.comm_info()["kind"] == "none":
         library_comm()
     info = ctx.comm_info()
-    factor = default_step_factor(args.config, "network", args.hidden_bf16, L)
+    factor = default_step_factor(args.config, "network", args.hidden_bf16, L, args.network_step_rule)
     ctx.set_launch_timing(True)
     if dist is not None:
         dist.barrier()
@@ -296,7 +306,8 @@ def main():
 
     n, M_total, B_total, widths = CONFIGS[args.config]
     if args.step_factor is None:
-        args.step_factor = default_step_factor(args.config, args.sampler, args.hidden_bf16, args.steps)
+        args.step_factor = default_step_factor(args.config, args.sampler, args.hidden_bf16, args.steps,
+                                               args.network_step_rule)
     heavy = widths[0] > 32   # gx-path configs: minutes of CPU per branch-step at full size
     if args.cpu_sample_branches is None:
         args.cpu_sample_branches = 4 if heavy else 96

@@ -1041,7 +1041,7 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
     allidx.insert(allidx.end(), h.snp_idx.begin(), h.snp_idx.end());
     for (int c = 0; c < h.dev.nchunks; ++c)
       jobs.push_back(PackJob{h.dev.x_off + 1024ll * c, 1024ll * h.dev.nchunks, base + 64 * c,
-                             std::min(64, h.m - 64 * c)});
+                             std::min(64, h.m - 64 * c), tile_f3m1(h.dev.fused) ? 1 : 0});
   }
   int32_t* d_idx = nullptr;
   PackJob* d_jobs = nullptr;

@@ -10,7 +10,7 @@
 #define BANN_WIDE_MAXCH 2    // wide fused kernel: m_b <= 128
 #define BANN_FX_MAXCH 8      // fx: <= 8 marker chunks of 64 (m_b <= 512), one wave per tile
 #define BANN_FXL_MAXCH 64    // fxl: <= 64 chunks (m_b <= 4096), one wave per <= 8-chunk block
-#define BANN_MAX_TILES_PER_WAVE 4096  // int32 dW0 digit sums: < 2^31 / (3.9e5 per tile)
+#define BANN_MAX_TILES_PER_WAVE 4096  // int32 dW0 digit sums: < 2^31 / (4.4e5 per tile: 16 K slots x 255 x (2 + 8 + 32 + 64))
 #define BANN_CHUNK 64        // markers per chunk (one 16x16x64 i8 MFMA K-step)
 #define BANN_FRAG 16         // individuals per fragment (MFMA N)
 #define BANN_TILE_FRAGS 4    // fragments per fused-kernel tile (64 individuals)
@@ -148,7 +148,11 @@ struct PackJob {
   int64_t tile_stride;  // bytes per tile of the branch's image (1024 nchunks)
   int32_t idx_off;      // first of the chunk's rows in the concatenated marker-index list
   int32_t rows;         // valid rows (markers) of the chunk, <= 64; the rest are zero padding
+  int32_t f3m1;         // tile images only: field 3 (bits 6-7) stored as code - 1 (fx / fxl / fxh branches)
 };
+// the fx / fxl / fxh kernels read their tile images with field 3 stored as code - 1
+// (kernels_fx.hip header); the wide and layered kernels read plain codes
+__host__ __device__ inline bool tile_f3m1(int fused) { return fused == 1 || fused == 3; }
 // genotype image: 2-bit variant-major rows of rowb = ceil(n/64)*16 bytes (kernels_data.hip header)
 void launch_synthetic_genotypes(uint8_t* raw, int64_t rowb, float* mu, float* sigma, int64_t n, int64_t M,
                                 uint64_t seed, hipStream_t s);

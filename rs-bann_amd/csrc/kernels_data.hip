@@ -259,6 +259,10 @@ __global__ void __launch_bounds__(256) k_pack_tiles(const uint8_t* __restrict__ 
     // its two 8-byte halves swapped at positions >= 8 (the parity of w is the global one: 4 windows per chunk)
     const int w = r >> 4, P = ((r & 15) + 8 * (w & 1)) & 15;
     uint4 v = s[tt][r];
+    if (jb.f3m1) {  // field 3 as code - 1 (codes <= 2: 0 -> 11, 1 -> 00, 2 -> 01; padding rows too)
+      auto f3 = [](uint32_t x) { return (x & 0x3F3F3F3Fu) | (((((x >> 6) & 0x03030303u) + 0x03030303u) & 0x03030303u) << 6); };
+      v = make_uint4(f3(v.x), f3(v.y), f3(v.z), f3(v.w));
+    }
     if (P >= 8) v = make_uint4(v.z, v.w, v.x, v.y);
     *reinterpret_cast<uint4*>(dst + jb.dst + (t0 + tt) * jb.tile_stride + (16 * w + P) * 16) = v;
   }

@@ -17,12 +17,13 @@
 // P = ((r & 15) + 8 (w & 1)) & 15, the 8-byte halves swapped for P >= 8
 // (k_pack_tiles, kernels_data.hip); byte (i & 63) >> 2 holds individuals 4q..4q+3
 __device__ __forceinline__ int tile_genotype(const uint8_t* __restrict__ img, int64_t tile_stride, int64_t i,
-                                             int j) {
+                                             int j, bool f3m1) {
   const int c = j >> 6, r = j & 63, w = r >> 4;
   const int P = ((r & 15) + 8 * (w & 1)) & 15;
   const int ii = (int)(i & 63), q = ii >> 2;
   const int64_t at = (i >> 6) * tile_stride + 1024 * c + (16 * w + P) * 16 + (P >= 8 ? (q ^ 8) : q);
-  return (img[at] >> (2 * (ii & 3))) & 3;
+  const int v = (img[at] >> (2 * (ii & 3))) & 3;
+  return (f3m1 && (ii & 3) == 3) ? ((v + 1) & 3) : v;  // field 3 stored as code - 1 (tile_f3m1)
 }
 
 // Z0 = X W0 + b0 with X = (g - mu) / sigma (bed.rs:325-355; sigma = 0 markers contribute 0)
@@ -38,12 +39,13 @@ __global__ void __launch_bounds__(FEED_T) k_feed0(DevState st, int b, float* __r
   const float* sg = st.sigma + bd.mk_off;
   const uint8_t* img = st.xu2 + bd.x_off;
   const int64_t tstride = 1024 * (int64_t)bd.nchunks;
+  const bool f3m1 = tile_f3m1(bd.fused);
   float acc[FEED_KB];
 #pragma unroll
   for (int kk = 0; kk < FEED_KB; ++kk) acc[kk] = 0.f;
   for (int j = 0; j < m; ++j) {
     const float s = sg[j];
-    const float x = s > 0.f ? ((float)tile_genotype(img, tstride, i, j) - mu[j]) / s : 0.f;
+    const float x = s > 0.f ? ((float)tile_genotype(img, tstride, i, j, f3m1) - mu[j]) / s : 0.f;
 #pragma unroll
     for (int kk = 0; kk < FEED_KB; ++kk)
       if (k0 + kk < w0) acc[kk] = fmaf(x, W[(int64_t)(k0 + kk) * m + j], acc[kk]);

@@ -39,6 +39,7 @@
 //     at a 4^p smaller scale, so the MFMA sum is unchanged.  The delta0 digit
 //     operand A is written in the same K order.
 #include <stdlib.h>
+#include <type_traits>
 
 #include "activations.h"
 #include "bann_internal.h"
@@ -56,6 +57,17 @@
 // p7 loop cycles.  FX_ABL (results wrong, timing only): 1 forward without the 2-bit unpack, 2 backward
 // without it, 4 no head (delta0 = z0), 8 no MFMAs (the operands XORed into the accumulators), 16 no
 // genotype / target stream (the loop computes on whatever the slots hold).
+//
+// Field 3 of every fx / fxl / fxh tile image is stored as code - 1 (k_pack_tiles, PackJob::f3m1):
+// read as a signed int8, a genotype byte is then f0 + 4 f1 + 16 f2 + 64 (f3 - 1) (codes <= 2, so
+// the 2-bit field holds -1 .. 1).  The forward takes CUMULATIVE fragments -- x & 0x03, x & 0x0F,
+// x & 0x3F and the raw byte: 3 ANDs per dword instead of 5 -- and recovers the in-place fields
+// exactly in int32 once per tile: F1 = C1 - C0, F2 = C2 - C1, F3 = C3 - C2 with C3 started at
+// 64 sum_k A (the W0-digit row sums over the wave's chunks, fx_rowsum64), so F_q = 4^q S_q as
+// before and z keeps its bits.  The backward keeps field 3 in place too (x & 0xC0 = 64 (f3 - 1):
+// one AND instead of a shift and an AND), with the delta0 digits of K-group 3 pre-divided by 64;
+// the -1 comes back as 64 sum_(i in group 3) digit_i, one MFMA per tile against FX_ONES3, added
+// to every marker's digit sums at the end.
 #ifndef FX_STAMPS
 #define FX_STAMPS 0
 #endif
@@ -83,10 +95,34 @@
 // is issued into tile t's slot as soon as tile t's backward has read chunk c's
 // last window (the target piece once the head has read the target), so a piece
 // has a whole tile more to land than when it is issued in the forward (the
-// one-tile-ahead and burst variants are profiling builds:
-// tools/profiling/kernels_fx_ablate.hip)
+// one-tile-ahead and burst variants measured slower: DESIGN.md 4)
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+#define FX_ONES3 (v4i{0, 0, 0, 0x40404040})  // 64 in every K slot of field 3 (the backward's group 3)
+
+// one chunk of the forward: the four cumulative fragments of a quad-byte operand
+__device__ __forceinline__ void fx_fwd_chunk(v4i A, v4u X, v4i (&facc)[4]) {
+  facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, (v4i)(X & 0x03030303u), facc[0], 0, 0, 0);
+  facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, (v4i)(X & 0x0F0F0F0Fu), facc[1], 0, 0, 0);
+  facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, (v4i)(X & 0x3F3F3F3Fu), facc[2], 0, 0, 0);
+  facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, (v4i)X, facc[3], 0, 0, 0);
+}
+// cumulative sums -> in-place fields F_q = 4^q S_q (facc[3] started at fx_rowsum64)
+__device__ __forceinline__ void fx_fwd_fields(v4i (&facc)[4]) {
+  facc[3] -= facc[2];
+  facc[2] -= facc[1];
+  facc[1] -= facc[0];
+}
+// 64 sum_k A[.][k] for the digit operands of chunks [0, nc): facc[3]'s start
+__device__ __forceinline__ v4i fx_rowsum64_acc(v4i A, v4i acc) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(A, v4i{0x40404040, 0x40404040, 0x40404040, 0x40404040}, acc, 0, 0, 0);
+}
+// the backward's fragments of one window dword: every field in place (x 1, 4, 16, and
+// 64 (f3 - 1)); the delta0 digits of K-group p carry 4^-p (p = 3: 64^-1)
+__device__ __forceinline__ v4i fx_bwd_unpack(uint32_t wv) {
+  return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u), (int)(wv & 0xC0C0C0C0u)};
+}
 
 __device__ __forceinline__ float ufl(float v) {  // make a wave-uniform value scalar
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
@@ -131,6 +167,12 @@ __device__ __forceinline__ float comb4_exact(v4i G) {
   const int64_t N = (int64_t)G[0] + ((int64_t)G[1] << 8) + ((int64_t)G[2] << 16) + ((int64_t)G[3] << 24);
   return (float)N;
 }
+// the same for two digit-sum vectors (a window's sums and the item's K-group-3 correction)
+__device__ __forceinline__ float comb4_exact2(v4i G, v4i H) {
+  const int64_t N = (int64_t)G[0] + ((int64_t)G[1] << 8) + ((int64_t)G[2] << 16) + ((int64_t)G[3] << 24) +
+                    (int64_t)H[0] + ((int64_t)H[1] << 8) + ((int64_t)H[2] << 16) + ((int64_t)H[3] << 24);
+  return (float)N;
+}
 
 // value(G) * 2^-sh for digit sums G, sh >= 0: form N in int64 (|G_d| < 2^31),
 // shift it, and re-split into 8-bit digits (exact up to the dropped low bits, < 1
@@ -152,16 +194,6 @@ __device__ __forceinline__ void swap16(float& a, float& b) {
                                                   false, false);
   a = __builtin_bit_cast(float, (unsigned)r[0]);
   b = __builtin_bit_cast(float, (unsigned)r[1]);
-}
-
-#ifndef FX_FWDPIPE
-#define FX_FWDPIPE 0
-#endif
-// forward fragment q of a 16-marker quad-byte operand: field q of every byte, in place
-// (x 4^q, folded into the digit combine) except q = 3 (bits 6-7 would overflow int8)
-__device__ __forceinline__ v4i fx_field(v4u x, int q) {
-  return q == 0 ? (v4i)(x & 0x03030303u)
-                : q == 1 ? (v4i)(x & 0x0C0C0C0Cu) : q == 2 ? (v4i)(x & 0x30303030u) : (v4i)((x >> 2u) & 0x30303030u);
 }
 
 // NCH: 8 = every branch of the launch has exactly 8 chunks (no per-chunk guards,
@@ -219,6 +251,8 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+  v4i rowsum64 = v4i{0, 0, 0, 0};  // the forward's facc[3] start (field 3 stored as code - 1)
+  for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
   // head weights as wave-uniform values: scalar registers for the whole item (the
   // per-tile LDS broadcasts serialised the head on their latencies)
   float uW[NL][4][4], uB[NH][4];
@@ -250,14 +284,13 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   const bool net_err = st.nete != nullptr;
   const float* ybr = net_err ? st.nete : st.y + bd.y_off;
   float* predb = st.pred + bd.y_off;
-  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   const int64_t tile_bytes = (int64_t)nch * 1024;
-#if FX_ABL & 128
+  // the stream's base in scalar registers: each piece is one global_load_lds in the saddr
+  // form (one address VGPR, no 64-bit address arithmetic per piece: -0.7 % per launch)
   const uint64_t xb = (uint64_t)(uintptr_t)(reinterpret_cast<const char*>(st.xu2) + bd.x_off);
   const char* xbase_s = reinterpret_cast<const char*>(
       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(xb >> 32)) << 32) |
       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)xb));
-#endif
 
   // LDS-DMA of the NEXT tile is spread over the current tile's forward phase
   // (one 1 KiB piece per chunk, the target piece in the head): issued in one
@@ -271,12 +304,8 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   auto issue_chunk = [&](int tt, int sl, int c) {
     if (FX_ABL & 16) return;
     if (c == nch - 1 && pad_row) return;
-#if FX_ABL & 128
     glds16_s(xbase_s + (uint64_t)tt * (uint64_t)tile_bytes + (uint64_t)(c * 1024), (uint32_t)lane * 16u,
              &s_x[wave][sl][c * 1024]);
-#else
-    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
-#endif
   };
   auto issue_y = [&](int tt, int sl) {
     if (FX_ABL & 16) return;
@@ -288,6 +317,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   v4i acc[32];  // dW0 digit sums per 16-marker window u (lane: column g, marker 16u + i16)
 #pragma unroll
   for (int u = 0; u < 32; ++u) acc[u] = v4i{0, 0, 0, 0};
+  v4i acc3 = v4i{0, 0, 0, 0};  // 64 sum over K-group 3 of the digits: field 3's -1, every marker
   int R[4] = {0, 0, 0, 0};  // running delta0 scale exponent per column (0 = unset)
   double rss = 0.0;
   float db[NH][4], dWo[4];
@@ -312,14 +342,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   if (tt < te) {
     for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
-    if (tt + NW < te && !(FX_ABL & 64)) {
+    if (tt + NW < te) {
       for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
       issue_y(tt + NW, 1);
     }
   }
   for (; tt < te; tt += NW, sl ^= 1) {
-    const bool more = tt + NW < te && !(FX_ABL & 64);
-    const bool more2 = tt + 2 * NW < te && !(FX_ABL & 64);  // tile tt + 2 NW goes into this slot
+    const bool more = tt + NW < te;
+    const bool more2 = tt + 2 * NW < te;  // tile tt + 2 NW goes into this slot
     // tile tt (issued during tile tt - NW) has landed.  (An L2 prefetch of the
     // tile after it measured +3 %: with 8 waves/CU the L2 is already the DMA's
     // working set.)
@@ -333,7 +363,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // ---- forward: Z0 of 64 individuals, exact int32 over all chunks ----
     // (software pipelined: the LDS reads of chunk c + 1 fly while chunk c's
     // four MFMAs issue; sched barriers keep the compiler from hoisting more)
-    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
     // the forward at raised priority too (with the stream issued in the backward:
     // -1.2 % per launch, A/B on one box)
     __builtin_amdgcn_s_setprio(1);
@@ -350,40 +380,6 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
         }
       }
-#if FX_FWDPIPE
-      // chunk c + 1's unpack is interleaved with chunk c's MFMAs (one chunk ahead): an
-      // MFMA's operand was written a chunk earlier, so no MFMA waits on the VALU that
-      // produced it; each field register is rewritten right after the MFMA that read it
-      v4i Bf[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Bf[q] = fx_field(Xq[0], q);
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        if (NCH == 0 && c >= nch) continue;
-        const v4i Ac = Aq[c % FD];
-        const bool nxt = c + 1 < 8 && (NCH != 0 || c + 1 < nch);
-        const v4u Xn = Xq[(c + 1) % FD];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, Bf[q], facc[q], 0, 0, 0);
-          if (nxt) Bf[q] = fx_field(Xn, q);
-        }
-        // each MFMA, then the next chunk's field it frees (4 VALU; field 3: 8)
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {  // chunk c's registers are free: chunk c + 2
-          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
-          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#else
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         if (NCH == 0 && c >= nch) continue;
@@ -393,20 +389,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
           Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
           Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
         }
-        // fragment q = field q of every byte, kept in place (x 4^q, folded into the
-        // digit combine below) except q = 3 (bits 6-7 would overflow int8)
+        // the cumulative fragments x & 0x03, x & 0x0F, x & 0x3F, x (header)
 #if FX_ABL & 1
         const v4i B0 = (v4i)Xc, B1 = (v4i)Xc, B2 = (v4i)Xc, B3 = (v4i)Xc;
-#elif FX_ABL & 32
+#else
         const v4i B0 = (v4i)(Xc & 0x03030303u);
         const v4i B1 = (v4i)(Xc & 0x0F0F0F0Fu);
         const v4i B2 = (v4i)(Xc & 0x3F3F3F3Fu);
         const v4i B3 = (v4i)Xc;
-#else
-        const v4i B0 = (v4i)(Xc & 0x03030303u);
-        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
-        const v4i B2 = (v4i)(Xc & 0x30303030u);
-        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
 #endif
         facc[0] = FX_MFMA(Ac, B0, facc[0]);
         facc[1] = FX_MFMA(Ac, B1, facc[1]);
@@ -414,35 +404,18 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         facc[3] = FX_MFMA(Ac, B3, facc[3]);
         __builtin_amdgcn_sched_barrier(0);
       }
-#endif
     }
     __builtin_amdgcn_sched_barrier(0);
     FX_STAMP(1);
-#if FX_ABL & 64
-    if (tt + NW < te) {  // one tile ahead, issued in the VALU-only head phase
-      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, sl ^ 1, c);
-      issue_y(tt + NW, sl ^ 1);
-    }
-#endif
     // the head + digit phase is a dependent VALU chain: at raised priority it
     // takes the SIMD's issue slots ahead of the partner wave's independent
     // MFMA/unpack stream (measured -1 %)
     __builtin_amdgcn_s_setprio(1);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
-#if FX_ABL & 32
-    float z0, z1, z2, z3;
-    {  // timing variant: cumulative fields solved in the float domain
-      const float c0 = comb4(facc[0]), c1 = comb4(facc[1]), c2 = comb4(facc[2]), c3 = comb4(facc[3]);
-      z0 = zscale * c0;
-      z1 = (0.25f * zscale) * (c1 - c0);
-      z2 = (0.0625f * zscale) * (c2 - c1);
-      z3 = fmaf(0.015625f * zscale, c3 - c2, zscale);
-    }
-#else
+    fx_fwd_fields(facc);  // F_q = 4^q S_q, exact
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
-    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
-#endif
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
     swap32(z0, z2);
     swap32(z1, z3);
     swap16(z0, z1);
@@ -564,11 +537,12 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 #pragma unroll
       for (int u = 0; u < 32; ++u)
         if (NCH != 0 || u < 4 * nch) acc[u] = shr_digits(acc[u], sh);
+      acc3 = shr_digits(acc3, sh);
     }
     v4u w;
     // this lane's individual sits in K-group p = g of the backward operand, whose
-    // genotype codes stay in place (x 4^p, p = 1, 2): pre-divide its digits by 4^p
-    const int kslot_sh = g == 1 ? 2 : g == 2 ? 4 : 0;
+    // genotype codes stay in place (x 4^p): pre-divide its digits by 4^p
+    const int kslot_sh = 2 * g;
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = digits4_fx(d[k], 153 - kslot_sh - (R[k] ? R[k] : 255));
     *reinterpret_cast<v4u*>(sd_w) = w;
@@ -578,17 +552,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     __builtin_amdgcn_s_setprio(0);
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
+    acc3 = FX_MFMA(A, FX_ONES3, acc3);
     {
-      // fields 1 and 2 in place (x 4, x 16; their delta digits carry 4^-p): 5 VALU
+      // every field in place (x 1, 4, 16, 64 (f3 - 1); the digits carry 4^-p): 4 VALU
       auto unpack = [](uint32_t wv) -> v4i {
 #if FX_ABL & 2
         return v4i{(int)wv, (int)wv, (int)wv, (int)wv};
-#elif FX_ABL & 512
-        return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
-                   (int)(wv & 0xC0C0C0C0u)};  // timing variant: field 3 in place (code - 1 storage)
 #else
-        return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
-                   (int)((wv >> 6) & 0x03030303u)};
+        return fx_bwd_unpack(wv);
 #endif
       };
       // window u + 2 is unpacked beside window u's MFMA: the MFMA's B operand was
@@ -654,7 +625,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     float* red = reinterpret_cast<float*>(&s_x[wave][0][0]);
 #pragma unroll
     for (int u = 0; u < 32; ++u)
-      if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4_exact(acc[u]), Rl - 153) : 0.f;
+      if (u < 4 * nch) red[u * 64 + lane] = Rl ? __builtin_amdgcn_ldexpf(comb4_exact2(acc[u], acc3), Rl - 153) : 0.f;
   }
   __syncthreads();
   float* part = st.part + it.part_at;
@@ -860,6 +831,8 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
+  v4i rowsum64 = v4i{0, 0, 0, 0};  // facc[3]'s start (field 3 stored as code - 1)
+  for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
   float uWm[NL][4][4], uB[NH][4];  // head weights W_l[j][k] (l >= 1; output layer: k = 0) and biases, scalar
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
@@ -898,7 +871,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
     for (int j = 1; j < NS; ++j) ahead += tt + j * NW < te;
     vm_wait_n(ahead * nch);
     const char* xs = &s_x[wave][sl][0];
-    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}};
+    v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
     {
       constexpr int FD = 2;
       v4u Xq[FD];
@@ -912,40 +885,6 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
           Aq[c] = *reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]);
         }
       }
-#if FX_FWDPIPE
-      // chunk c + 1's unpack is interleaved with chunk c's MFMAs (one chunk ahead): an
-      // MFMA's operand was written a chunk earlier, so no MFMA waits on the VALU that
-      // produced it; each field register is rewritten right after the MFMA that read it
-      v4i Bf[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Bf[q] = fx_field(Xq[0], q);
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        if (NCH == 0 && c >= nch) continue;
-        const v4i Ac = Aq[c % FD];
-        const bool nxt = c + 1 < 8 && (NCH != 0 || c + 1 < nch);
-        const v4u Xn = Xq[(c + 1) % FD];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          facc[q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, Bf[q], facc[q], 0, 0, 0);
-          if (nxt) Bf[q] = fx_field(Xn, q);
-        }
-        // each MFMA, then the next chunk's field it frees (4 VALU; field 3: 8)
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-        if (c + FD < 8 && (NCH != 0 || c + FD < nch)) {  // chunk c's registers are free: chunk c + 2
-          Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
-          Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#else
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         if (NCH == 0 && c >= nch) continue;
@@ -955,21 +894,14 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
           Xq[c % FD] = (v4u)lds_tr8_pair(xs + (c + FD) * 1024 + fo0, xs + (c + FD) * 1024 + fo1);
           Aq[c % FD] = *reinterpret_cast<const v4i*>(&s_w0[(c + FD) * 1024 + lane * 16]);
         }
-        const v4i B0 = (v4i)(Xc & 0x03030303u);
-        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
-        const v4i B2 = (v4i)(Xc & 0x30303030u);
-        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
-        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B0, facc[0], 0, 0, 0);
-        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B1, facc[1], 0, 0, 0);
-        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B2, facc[2], 0, 0, 0);
-        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Ac, B3, facc[3], 0, 0, 0);
+        fx_fwd_chunk(Ac, Xc, facc);
         __builtin_amdgcn_sched_barrier(0);
       }
-#endif
     }
     __builtin_amdgcn_sched_barrier(0);
+    fx_fwd_fields(facc);
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
-    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
     swap32(z0, z2);
     swap32(z1, z3);
     swap16(z0, z1);
@@ -1052,6 +984,10 @@ void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems
 // registers two chunks ahead with counted loads instead of an LDS image.
 // ===========================================================================
 #define FXL_MAXW 8
+// k_fused_grad_fxh (below)
+#define FXH_CPW 5   // chunks per compute wave (at most)
+#define FXH_MAXC 7  // compute waves (+ the head wave: 8 waves)
+#define FXH_NSL 4   // genotype slots per compute wave
 #ifndef FXL_PD
 #define FXL_PD 8  // backward genotype-window prefetch depth
 #endif
@@ -1209,6 +1145,23 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 #pragma unroll
     for (int c = 0; c < CPW; ++c) asm volatile("" : "+v"(Dres[c]));  // landed: no compiler waits in the loop
   }
+  // field 3 stored as code - 1: z3 = (s / 64) comb4(C3 - C2) + s comb4(sum_k A) over the
+  // wave's block (the float form: fxl's partials are f32 anyway, and an int32 start value
+  // would take 4 more VGPRs in the counted 8-chunk waves)
+  float zrow;
+  {
+    v4i rs = v4i{0, 0, 0, 0};
+    if constexpr (RES) {
+#pragma unroll
+      for (int c = 0; c < CPW; ++c)
+        if (FULL || c < cw) rs = fx_rowsum64_acc(Dres[c], rs);
+    } else {
+      for (int c = 0; c < cw; ++c) rs = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(dsrc + c * 1024), rs);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    zrow = (0.015625f * zscale) * comb4(rs);
+    asm volatile("" : "+v"(zrow));
+  }
   if (tt < te) {
     for (int c = 0; c < cw; ++c) issue_chunk(tt, 0, c);
     issue_y(tt, 0);
@@ -1259,22 +1212,16 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
           issue_chunk(tt + 1, sl ^ 1, c);
         else if (CNT)  // last tile: a harmless L2-resident DMA keeps the counts fixed
           glds16(dsrc + c * 1024, xslot0 + (sl ^ 1) * SLOT + c * 1024);
-        const v4i B0 = (v4i)(Xc & 0x03030303u);
-        const v4i B1 = (v4i)(Xc & 0x0C0C0C0Cu);
-        const v4i B2 = (v4i)(Xc & 0x30303030u);
-        const v4i B3 = (v4i)((Xc >> 2u) & 0x30303030u);
-        facc[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B0, facc[0], 0, 0, 0);
-        facc[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B1, facc[1], 0, 0, 0);
-        facc[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B2, facc[2], 0, 0, 0);
-        facc[3] = __builtin_amdgcn_mfma_i32_16x16x64_i8(Dg[c], B3, facc[3], 0, 0, 0);
+        fx_fwd_chunk(Dg[c], Xc, facc);
         __builtin_amdgcn_sched_barrier(0);
         Xc = Xn;
       }
     }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    fx_fwd_fields(facc);  // F3 = 64 S3 - 64 sum_k A: zrow adds the latter back
     float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
-    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.0625f * zscale) * comb4(facc[3]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = fmaf(0.015625f * zscale, comb4(facc[3]), zrow);
     swap32(z0, z2);
     swap32(z1, z3);
     swap16(z0, z1);
@@ -1405,9 +1352,11 @@ __global__ void __launch_bounds__(64 * FXL_MAXW, 1)
 #pragma unroll
       for (int u = 0; u < PD; ++u)
         wq[u] = (FULL || u < 4 * cw) ? *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe)) : 0u;
+      // field 3 (stored as code - 1) decoded: ((x >> 6) + 1) & 3 per byte (fields 0-2 hold
+      // codes <= 2, so the +1 never carries out of a byte)
       auto unpack = [](uint32_t wv) -> v4i {
         return v4i{(int)(wv & 0x03030303u), (int)(wv & 0x0C0C0C0Cu), (int)(wv & 0x30303030u),
-                   (int)((wv >> 6) & 0x03030303u)};
+                   (int)(((wv >> 6) + 0x01010101u) & 0x03030303u)};
       };
       v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);  // two windows ahead of their MFMA (as in fx)
 #pragma unroll
@@ -1526,9 +1475,20 @@ int fxl_cpw(int nchunks) {
 
 // nw waves per workgroup (= ceil(chunks / cpw) of every branch of the launch);
 // full: every branch has exactly cpw * nw chunks
+bool fxh_takes(int nw, int cpw);
+template <int NL>
+static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
+                          hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                            int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s) {
   if (nitems <= 0 || nw < 1 || nw > FXL_MAXW || (cpw != 4 && cpw != 8)) return;
+  if (fxh_takes(nw, cpw) && L >= 2 && L <= 4) {  // the head-wave kernel: ceil(4 nw / 5) compute waves
+    const int nc = (4 * nw + FXH_CPW - 1) / FXH_CPW;
+    if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, nc, write_pred, s);
+    if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, nc, write_pred, s);
+    if (L == 4) launch_fxh_nl<4>(st, items, nitems, act, nc, write_pred, s);
+    return;
+  }
   switch (L * 4 + (full ? 2 : 0) + (cpw == 4 ? 1 : 0)) {
     case 8: launch_fxl_nl<2, 0, 8>(st, items, nitems, act, nw, write_pred, s); break;
     case 9: launch_fxl_nl<2, 0, 4>(st, items, nitems, act, nw, write_pred, s); break;
@@ -1544,4 +1504,455 @@ void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t ni
     case 19: launch_fxl_nl<4, 1, 4>(st, items, nitems, act, nw, write_pred, s); break;
     default: break;
   }
+}
+
+// ===========================================================================
+// k_fused_grad_fxh: fxl's one-tile-at-a-time scheme with the head in ONE wave.
+//
+// fxl repeats the head (hidden / summary / output layers, e, rss, delta0 and
+// its digits) in every wave of the workgroup: at C2 (32 chunks, 8 waves) that
+// is 8 x ~300 VALU per tile against 8 x 160 for the 2-bit unpack.  Here wave 0
+// is the HEAD wave and waves 1 .. NC are COMPUTE waves owning <= 5 chunks each
+// (C2: 7 waves of 5,5,5,5,4,4,4), software-pipelined two tiles deep with ONE
+// workgroup barrier per phase p:
+//   compute waves: backward of tile p - 2 (its delta0 digits published by the
+//                  head wave in phase p - 1), then the LDS-DMA of tile
+//                  p + NSL - 2 into the slot just freed, then the forward of
+//                  tile p -> partial Z0 (f32, the per-column scale applied)
+//                  into the exchange slot p % 2;
+//   head wave:     the fixed-order sum of the NC partials of tile p - 1, the
+//                  transpose to one individual per lane, the head, the delta0
+//                  digits at the running per-column scale -> digit image
+//                  (p - 1) % 2, with the scale shifts for the compute waves'
+//                  digit sums.
+// A tile stays resident in its compute waves' slots from its forward (phase
+// p) to its backward (p + 2): NSL = 4 slots per wave (one tile two phases
+// ahead in flight), 157 KiB of LDS at NC = 7: one workgroup per CU, two waves
+// per SIMD, the head wave sharing its SIMD with one compute wave.
+// Arithmetic per tile is fxl's (the same digits, int32 digit sums, head in
+// f32); the Z0 partials are summed in compute-wave order, so the bits differ
+// from fxl only through the partition of the chunks over waves.
+// ===========================================================================
+
+int fxh_lds_bytes(int nc, int nl) {
+  const int ns = 8 + (nl - 2) * 20;
+  return nc * FXH_NSL * FXH_CPW * 1024 + 2 * nc * 64 * 16 + 2 * 4 * FX_DROW + 3 * 64 * 4 + 16 * 4 + nl * 20 * 4 +
+         ns * 4 + 4 * 4;
+}
+
+template <int NL, int ACT>
+__global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
+    k_fused_grad_fxh(DevState st, const GradItem* __restrict__ items, int write_pred) {
+  constexpr int NH = NL - 1;
+  constexpr int NS = 8 + (NH - 1) * 20;
+  constexpr int CPW = FXH_CPW, SLOT = CPW * 1024, NSL = FXH_NSL;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int NC = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6) - 1);
+  char* const s_x = lds;                                                // [NC][NSL][SLOT]
+  v4f* const s_zx = reinterpret_cast<v4f*>(s_x + NC * NSL * SLOT);      // [2][NC][64]
+  char* const s_d = reinterpret_cast<char*>(s_zx + 2 * NC * 64);        // [2][4 * FX_DROW]
+  float* const s_y = reinterpret_cast<float*>(s_d + 2 * 4 * FX_DROW);   // [3][64]
+  int* const s_sc = reinterpret_cast<int*>(s_y + 3 * 64);               // [2][8]: shift[4], R[4]
+  float* const s_hw = reinterpret_cast<float*>(s_sc + 16);              // [NL][20]
+  float* const s_hs = s_hw + NL * 20;                                   // [NS]
+  float* const s_db0 = s_hs + NS;                                       // [4]
+
+  const GradItem it = items[blockIdx.x];
+  const int b = it.branch;
+  const BranchDev& bd = st.br[b];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t n = st.n;
+  const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
+  const int T = te > tb ? te - tb : 0;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
+  float* const part = st.part + it.part_at;
+
+  if (wave == 0) {
+    // ================= head wave =================
+    const float* th = st.theta + bd.p_off;
+    for (int t = lane; t < NL * 20; t += 64) {
+      const int l = t / 20, r = t - l * 20;
+      float v = 0.f;
+      if (r < 16) {
+        const int j = r >> 2, k = r & 3;
+        if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+      } else {
+        const int k = r - 16;
+        if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+        if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+      }
+      s_hw[t] = v;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    float uW[NL][4][4], uB[NH][4];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          uW[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l * 20 + 4 * j + k]) : 0.f;
+      if (l < NH)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l * 20 + 16 + k]);
+    }
+    const int iota = 4 * i16 + g;
+    const float* ybr = st.y + bd.y_off;
+    float* predb = st.pred + bd.y_off;
+    auto issue_y = [&](int k) {
+      const int64_t row = 64 * (int64_t)(tb + k) + iota;
+      glds4(ybr + (row < n ? row : n - 1), s_y + (k % 3) * 64);
+    };
+    if (T > 0) issue_y(0);
+    if (T > 1) issue_y(1);
+    const int wp = write_pred != 0;
+    const int kslot_sh = 2 * g;  // K-group g's genotype field in place (x 4^g): digits pre-divided
+    int R[4] = {0, 0, 0, 0};
+    double rss = 0.0;
+    float db[NH][4], dWo[4];
+    float dW[NL > 2 ? NL - 2 : 1][4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      dWo[k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < NH; ++l) db[l][k] = 0.f;
+#pragma unroll
+      for (int l = 0; l < (NL > 2 ? NL - 2 : 1); ++l)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dW[l][j][k] = 0.f;
+    }
+    for (int p = 0; p < T + 2; ++p) {
+      if (p >= 1 && p <= T) {
+        const int k = p - 1;
+        // y(k) has landed: younger are store(k - 2), y(k + 1), store(k - 1)
+        vm_wait_n(wp * (k >= 2) + (k + 1 < T) + wp * (k >= 1));
+        __builtin_amdgcn_s_setprio(1);
+        // the NC partials in compute-wave order; all FXH_MAXC slots read (past NC they are
+        // other LDS bytes, not added), so the loads issue together
+        const v4f* xz = s_zx + (k & 1) * NC * 64 + lane;
+        v4f zp[FXH_MAXC];
+#pragma unroll
+        for (int w = 0; w < FXH_MAXC; ++w) zp[w] = xz[w * 64];
+        v4f zs = zp[0];
+#pragma unroll
+        for (int w = 1; w < FXH_MAXC; ++w)
+          if (w < NC) zs += zp[w];
+        float z0 = zs[0], z1 = zs[1], z2 = zs[2], z3 = zs[3];
+        swap32(z0, z2);
+        swap32(z1, z3);
+        swap16(z0, z1);
+        swap16(z2, z3);
+        const int64_t row = 64 * (int64_t)(tb + k) + iota;
+        const bool valid = row < n;
+        const float yv = s_y[(k % 3) * 64 + lane];
+        if (k + 2 < T) issue_y(k + 2);  // slot (k + 2) % 3 = (k - 1) % 3, read in the previous phase
+        float d[4];
+        {
+          float z[NH][4], a[NH][4];
+          z[0][0] = z0 + uB[0][0];
+          z[0][1] = z1 + uB[0][1];
+          z[0][2] = z2 + uB[0][2];
+          z[0][3] = z3 + uB[0][3];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[0][q] = act_h_t<ACT>(z[0][q]);
+#pragma unroll
+          for (int l = 1; l < NH; ++l) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              float s = uB[l][q];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) s = fmaf(a[l - 1][j], uW[l][j][q], s);
+              z[l][q] = s;
+              a[l][q] = act_h_t<ACT>(s);
+            }
+          }
+          float out = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], uW[NL - 1][j][0], out);
+          const float e = valid ? out - yv : 0.f;
+          rss += (double)e * (double)e;
+          float err[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            dWo[j] = fmaf(a[NH - 1][j], e, dWo[j]);
+            err[j] = e * uW[NL - 1][j][0];
+          }
+#pragma unroll
+          for (int l = NH - 1; l >= 0; --l) {
+            float dl[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              dl[q] = act_dh_t<ACT>(z[l][q], a[l][q]) * err[q];
+              db[l][q] += dl[q];
+            }
+            if (l >= 1) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                float sj = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  dW[l - 1][j][q] = fmaf(a[l - 1][j], dl[q], dW[l - 1][j][q]);
+                  sj = fmaf(dl[q], uW[l][j][q], sj);
+                }
+                err[j] = sj;
+              }
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) d[q] = dl[q];
+            }
+          }
+          if (wp && valid) predb[row] = out;
+        }
+        // delta0 -> signed digits at the running per-column scale (fxl's rule)
+        int sh[4] = {0, 0, 0, 0};
+        {
+          bool lane_need = false;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int eq = (int)((fbits(d[q]) >> 23) & 0xFFu);
+            lane_need |= eq > (R[q] ? R[q] : 5);
+          }
+          if (__builtin_amdgcn_ballot_w64(lane_need) != 0) {
+            const uint32_t e01 =
+                wave_max_u16x2(((fbits(d[0]) >> 23) & 0xFFu) | (((fbits(d[1]) >> 23) & 0xFFu) << 16));
+            const uint32_t e23 =
+                wave_max_u16x2(((fbits(d[2]) >> 23) & 0xFFu) | (((fbits(d[3]) >> 23) & 0xFFu) << 16));
+            const int E[4] = {(int)(e01 & 0xFFFFu), (int)(e01 >> 16), (int)(e23 & 0xFFFFu), (int)(e23 >> 16)};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              if (E[q] >= 6 && (R[q] == 0 || E[q] > R[q])) {
+                if (R[q] != 0) sh[q] = E[q] + 2 - R[q];
+                R[q] = E[q] + 2;
+              }
+            }
+          }
+        }
+        v4u w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = digits4_fx(d[q], 153 - kslot_sh - (R[q] ? R[q] : 255));
+        char* const sd = s_d + (k & 1) * 4 * FX_DROW;
+        *reinterpret_cast<v4u*>(sd + (i16 >> 2) * FX_DROW + (4 * g + (i16 & 3)) * 16) = w;
+        if (lane == 0) {
+          *reinterpret_cast<v4i*>(s_sc + (k & 1) * 8) = v4i{sh[0], sh[1], sh[2], sh[3]};
+          *reinterpret_cast<v4i*>(s_sc + (k & 1) * 8 + 4) = v4i{R[0], R[1], R[2], R[3]};
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+      LDS_BARRIER();
+    }
+    // head statistics -> the partial slab; sum delta0 per column for the compute waves
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double rs = wave_sum_d(rss);
+    float hs[NS];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hs[k] = wave_sum(db[0][k]);
+      hs[4 + k] = wave_sum(dWo[k]);
+    }
+#pragma unroll
+    for (int l = 1; l < NH; ++l)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hs[8 + (l - 1) * 20 + k] = wave_sum(db[l][k]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hs[8 + (l - 1) * 20 + 4 + 4 * j + k] = wave_sum(dW[l - 1][j][k]);
+      }
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q) s_hs[q] = hs[q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_db0[k] = hs[k];
+      st.rss_part[it.rss_at] = rs;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < NS) {
+      const float v = s_hs[lane];
+      const int q = lane;
+      if (q < 4) {
+        if (q < bd.widths[0]) part[bd.boff[0] + q] = v;
+      } else if (q < 8) {
+        const int j = q - 4;
+        if (j < bd.win[NL - 1]) part[bd.woff[NL - 1] + j] = v;
+      } else {
+        const int l = 1 + (q - 8) / 20, r = (q - 8) % 20;
+        if (r < 4) {
+          if (r < bd.widths[l]) part[bd.boff[l] + r] = v;
+        } else {
+          const int j = (r - 4) >> 2, k = (r - 4) & 3;
+          if (j < bd.win[l] && k < bd.widths[l]) part[bd.woff[l] + k * bd.win[l] + j] = v;
+        }
+      }
+    }
+    LDS_BARRIER();
+    return;
+  }
+
+  // ================= compute waves =================
+  const int cwi = wave - 1;
+  const int nch = bd.nchunks;
+  const int cbase = nch / NC, crem = nch - cbase * NC;
+  const int c0 = cwi * cbase + (cwi < crem ? cwi : crem);
+  const int cw = cbase + (cwi < crem ? 1 : 0);  // 1 .. CPW chunks of this wave
+  float zscale = st.fc[b].scale[g];
+  const uint32_t gsw = g & 1;
+  const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
+  const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
+  const int pe = i16, po = (i16 + 8) & 15;
+  const uint32_t boe = (uint32_t)(pe * 16 + 4 * (2 * ((g >> 1) ^ (pe >> 3)) + (g & 1)));
+  const uint32_t boo = (uint32_t)(po * 16 + 4 * (2 * ((g >> 1) ^ (po >> 3)) + (g & 1)));
+  const int64_t tile_bytes = (int64_t)nch * 1024;
+  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + (int64_t)c0 * 1024 + lane * 16;
+  const char* dsrc = reinterpret_cast<const char*>(st.dig) + bd.dig_off + (int64_t)c0 * 1024 + lane * 16;
+  char* const xslot0 = s_x + cwi * NSL * SLOT;
+  const char* const sd_r0 = s_d + g * FX_DROW + tq * 16 + 8 * tp;
+  // the chunk count as a compile-time constant (4 or 5 for every group fxh_takes: nch in
+  // (4 (nw - 1), 4 nw], NC = ceil(4 nw / 5)): no per-chunk / per-window guards, so each
+  // phase is one basic block the compiler schedules across (guards collapse the LDS
+  // prefetch distance to one window)
+  auto run = [&](auto cw_const) {
+    constexpr int CW = decltype(cw_const)::value, NWC = 4 * CW;
+    auto issue_tile = [&](int k) {
+      const int sl = k % NSL;
+#pragma unroll
+      for (int c = 0; c < CW; ++c)
+        glds16(xsrc + (int64_t)(tb + k) * tile_bytes + c * 1024, xslot0 + sl * SLOT + c * 1024);
+    };
+    v4i Dres[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) Dres[c] = *reinterpret_cast<const v4i*>(dsrc + c * 1024);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < CW; ++c) asm volatile("" : "+v"(Dres[c]));
+    asm volatile("" : "+v"(zscale));
+    v4i rowsum64 = v4i{0, 0, 0, 0};  // facc[3]'s start (field 3 stored as code - 1)
+#pragma unroll
+    for (int c = 0; c < CW; ++c) rowsum64 = fx_rowsum64_acc(Dres[c], rowsum64);
+    for (int k = 0; k < NSL && k < T; ++k) issue_tile(k);  // every slot filled; tile k + NSL refills slot k in B(k)
+    v4i acc[NWC];
+#pragma unroll
+    for (int u = 0; u < NWC; ++u) acc[u] = v4i{0, 0, 0, 0};
+    v4i acc3 = v4i{0, 0, 0, 0};  // field 3's -1: 64 sum over K-group 3 of the digits, every marker
+    int Rg = 0;  // the running delta0 scale of this lane's column (published by the head wave)
+
+    for (int p = 0; p < T + 2; ++p) {
+      // ---- backward of tile p - 2: dW0 digit sums of this wave's chunks += G^T delta0 ----
+      if (p >= 2) {
+        const int k = p - 2;
+        const int* sc = s_sc + (k & 1) * 8;
+        const int sh = sc[g];
+        Rg = sc[4 + g];
+        if (__builtin_amdgcn_ballot_w64(sh != 0) != 0) {
+#pragma unroll
+          for (int u = 0; u < NWC; ++u) acc[u] = shr_digits(acc[u], sh);
+          acc3 = shr_digits(acc3, sh);
+        }
+        const char* sd_r = sd_r0 + (k & 1) * 4 * FX_DROW;
+        const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
+        acc3 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, FX_ONES3, acc3, 0, 0, 0);
+        const char* xs = xslot0 + (k % NSL) * SLOT;
+        const bool refill = k + NSL < T;  // tile k + NSL into this slot, chunk by chunk
+        const char* rsrc = xsrc + (int64_t)(tb + k + NSL) * tile_bytes;
+        constexpr int PD = FXL_PD < NWC ? FXL_PD : NWC;
+        uint32_t wq[PD];
+#pragma unroll
+        for (int u = 0; u < PD; ++u) wq[u] = *reinterpret_cast<const uint32_t*>(xs + 256 * u + ((u & 1) ? boo : boe));
+        auto unpack = [](uint32_t wv) -> v4i { return fx_bwd_unpack(wv); };
+        v4i Bn = unpack(wq[0]), Bn2 = unpack(wq[1]);
+#pragma unroll
+        for (int u = 0; u < NWC; ++u) {
+          const v4i Bv = Bn;
+          Bn = Bn2;
+          if (u + 2 < NWC) Bn2 = unpack(wq[(u + 2) % PD]);
+          if (u + PD < NWC)
+            wq[u % PD] = *reinterpret_cast<const uint32_t*>(xs + 256 * (u + PD) + (((u + PD) & 1) ? boo : boe));
+          acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bv, acc[u], 0, 0, 0);
+          // chunk u >> 2's last window (u | 3) was unpacked at u = 4c + 1: its LDS bytes are free
+          if ((u & 3) == 1) {
+            asm volatile("" ::"v"(Bn2));
+            if (refill) glds16(rsrc + (u >> 2) * 1024, xslot0 + (k % NSL) * SLOT + (u >> 2) * 1024);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // ---- forward of tile p: partial Z0 over this wave's chunks -> exchange slot p % 2 ----
+      if (p < T) {
+        // pieces younger than tile p's: tiles p + 1 .. min(max(p + NSL - 2, NSL - 1), T - 1) (the
+        // prologue's NSL tiles, then one refill per backward, tile p + NSL - 2 in phase p)
+        const int hi = p + NSL - 2 > NSL - 1 ? p + NSL - 2 : NSL - 1;
+        vm_wait_n(CW * ((hi < T - 1 ? hi : T - 1) - p));
+        const char* xs = xslot0 + (p % NSL) * SLOT;
+        v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
+        __builtin_amdgcn_s_setprio(1);
+        v4u Xc = (v4u)lds_tr8_pair(xs + fo0, xs + fo1);
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+          v4u Xn = Xc;
+          if (c + 1 < CW) Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
+          fx_fwd_chunk(Dres[c], Xc, facc);
+          __builtin_amdgcn_sched_barrier(0);
+          Xc = Xn;
+        }
+        fx_fwd_fields(facc);
+        const float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+        const float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
+        lds_st_v4f(s_zx + ((p & 1) * NC + cwi) * 64 + lane, v4f{z0, z1, z2, z3});
+        __builtin_amdgcn_s_setprio(0);
+      }
+      LDS_BARRIER();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LDS_BARRIER();  // the head wave's delta0 column sums
+    {  // this wave's markers: dW0 = (G^T delta0 - mu sum delta0) / sigma
+      const float dbc = s_db0[g];
+      const int m = bd.m;
+#pragma unroll
+      for (int u = 0; u < NWC; ++u) {
+        const int mk = 16 * (4 * c0 + u) + i16;
+        if (mk < m && g < bd.widths[0]) {
+          const float s = Rg ? __builtin_amdgcn_ldexpf(comb4_exact2(acc[u], acc3), Rg - 153) : 0.f;
+          const float mu = st.mu[bd.mk_off + mk], sg = st.sigma[bd.mk_off + mk];
+          part[bd.woff[0] + g * m + mk] = sg > 0.f ? (s - mu * dbc) / sg : 0.f;
+        }
+      }
+    }
+  };
+  if (cw == 5)
+    run(std::integral_constant<int, 5>{});
+  else
+    run(std::integral_constant<int, 4>{});
+}
+
+template <int NL>
+static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
+                          hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * (nc + 1));
+  const size_t shm = (size_t)fxh_lds_bytes(nc, NL);
+#define FXH_GO(A)                                                                                       \
+  do {                                                                                                  \
+    static bool attr_ = false;                                                                          \
+    if (!attr_) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)k_fused_grad_fxh<NL, A>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                fxh_lds_bytes(FXH_MAXC, 4));                                            \
+      attr_ = true;                                                                                     \
+    }                                                                                                   \
+    hipLaunchKernelGGL((k_fused_grad_fxh<NL, A>), grid, block, shm, s, st, items, wp);                  \
+  } while (0)
+  switch (act) {
+    case 0: FXH_GO(0); break;
+    case 1: FXH_GO(1); break;
+    case 2: FXH_GO(2); break;
+    case 3: FXH_GO(3); break;
+    default: FXH_GO(4); break;
+  }
+#undef FXH_GO
+}
+
+// the head-wave kernel for fxl groups of 4-chunk waves with >= 5 waves (17 .. 32
+// chunks); BANN_FXL_HEAD=0 keeps fxl (A/B)
+bool fxh_takes(int nw, int cpw) {
+  const char* e = getenv("BANN_FXL_HEAD");  // read per launch: tests switch it between contexts
+  return (!e || atoi(e) != 0) && cpw == 4 && nw >= 5 && nw <= 8;
 }

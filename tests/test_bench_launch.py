@@ -50,9 +50,12 @@ def test_step_factor_rule():
     assert abs(f("c3", "branch", False, 10) - 0.5) < 1e-12
     assert abs(f("c5", "branch", False, 10) - 0.05) < 1e-12 and abs(f("c5", "branch", False, 20) - 0.1) < 1e-12
     assert abs(f("c5", "branch", True, 10) - 0.01) < 1e-12
-    assert abs(f("c3", "network", False, 20) - 0.11) < 1e-12 and abs(f("c3", "network", False, 10) - 0.055) < 1e-12
+    assert abs(f("c3", "network", False, 20) - 0.5) < 1e-12 and abs(f("c3", "network", False, 10) - 0.25) < 1e-12
+    # without the common-mode step rule the joint state's stiff mode caps the factor
+    assert abs(f("c3", "network", False, 20, "off") - 0.11) < 1e-12
     assert abs(f("c3def", "branch", False, 4) - 0.008) < 1e-12 and f("c3def", "branch", False, 20) == 0.02
-    # C5's joint network state, tuned on MI355X (0.0005 accepts at L = 20, 0.001 rejects)
-    assert abs(f("c5", "network", False, 20) - 0.0005) < 1e-15 and abs(f("c5", "network", True, 20) - 0.0005) < 1e-15
+    # C5's joint network state, tuned on MI355X: 0.02 with the rule, 0.0005 without
+    assert abs(f("c5", "network", False, 20) - 0.02) < 1e-15 and abs(f("c5", "network", True, 20) - 0.01) < 1e-15
+    assert abs(f("c5", "network", False, 20, "off") - 0.0005) < 1e-15
     # an untuned line: the branch sampler's factor, one tenth for the joint network state
     assert abs(f("c2", "network", False, 20) - 0.1) < 1e-12

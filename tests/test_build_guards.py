@@ -45,11 +45,11 @@ def test_counted_fxl_instantiations_do_not_spill(tmp_path):
 
 
 def test_production_build_sets_no_profiling_switches():
-    """the fx kernel's profiling switches (FX_STAMPS phase stamps, FX_ABL ablations, FX_FWDPIPE
-    experiment; tools/build_ab.sh builds variant libraries with them) default to 0 in the source
+    """the fx kernel's profiling switches (FX_STAMPS phase stamps, FX_ABL ablations;
+    tools/build_ab.sh builds variant libraries with them) default to 0 in the source
     and the product build (Makefile, __graft_entry__.build) defines none of them"""
     txt = open(SRC).read()
-    for sw in ("FX_STAMPS", "FX_ABL", "FX_FWDPIPE"):
+    for sw in ("FX_STAMPS", "FX_ABL"):
         assert f"#ifndef {sw}\n#define {sw} 0\n#endif" in txt, sw
     mk = open(os.path.join(os.path.dirname(SRC), "Makefile")).read()
     entry = open(os.path.join(ROOT, "__graft_entry__.py")).read()

@@ -1127,3 +1127,56 @@ def test_fused_solo_hmc_step_bitwise(Ctx, monkeypatch, graph):
             assert np.array_equal(f0[k], f1[k]), k
         acc += int(s1[0] == 0)
     assert acc > 0
+
+
+def test_fxh_head_wave_kernel(Ctx):
+    """k_fused_grad_fxh (fxl shapes of 17..32 chunks: one head wave, compute waves
+    of <= 5 chunks, two-tile software pipeline): oracle gradients, rss and
+    predictions for ragged chunk partitions (18, 21, 27 and 32 chunks over 4..7
+    compute waves; 2, 3 and 4 layers), in solo plans (one or two tiles per item:
+    the pipeline's prologue / epilogue) and in long items (BANN_SOLO=0), packed
+    and one branch at a time; and fxl (BANN_FXL_HEAD=0) agrees to f32 rounding."""
+    rng = np.random.default_rng(41)
+    n = 3000
+    shapes = [(1100, [4, 4, 1], "tanh"), (1300, [3, 2, 1], "relu"), (1700, [4, 4, 4, 1], "silu"),
+              (2048, [4, 1], "tanh")]
+    M = sum(m for m, _, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w, a in shapes:
+        br = f32_branch(O.random_branch(rng, m, w, act=a))
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32), branch=br,
+                          y=rng.normal(size=n).astype(np.float32).astype(np.float64)))
+        off += m
+    res = {}
+    mu = sd = None
+    for mode, solo in (("1", None), ("1", "0"), ("0", "0")):
+        os.environ["BANN_FXL_HEAD"] = mode
+        if solo is not None:
+            os.environ["BANN_SOLO"] = solo
+        try:
+            ctx = build_context(Ctx, g, specs)
+            assert all(ctx.kernel_path(b) == "fused_large" for b in range(len(specs)))
+            mu, sd = ctx.genotype_stats()
+            many, rss_many = ctx.log_density_gradient_many(list(range(len(specs))))
+            single = [ctx.log_density_gradient(b) for b in range(len(specs))]
+            preds = [ctx.predict(b) for b in range(len(specs))]
+            again, _ = ctx.log_density_gradient_many(list(range(len(specs))))
+            ctx.close()
+        finally:
+            del os.environ["BANN_FXL_HEAD"]
+            os.environ.pop("BANN_SOLO", None)
+        for a, b_ in zip(many, again):
+            assert np.array_equal(a, b_)  # fixed-order reductions: bitwise reproducible
+        res[(mode, solo)] = (many, rss_many, single, preds)
+    for key, (many, rss_many, single, preds) in res.items():
+        for b, s in enumerate(specs):
+            X = x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]])
+            ogw, ogb, orss = O.log_density_gradient(s["branch"], X, s["y"])
+            ref = O.param_vec(ogw, ogb)
+            assert norm_rel(many[b], ref) < TOL, (key, b, norm_rel(many[b], ref))
+            assert norm_rel(single[b][0], ref) < TOL, (key, b)
+            assert scalar_close(rss_many[b], orss) and scalar_close(single[b][1], orss), (key, b)
+            assert norm_rel(preds[b], O.predict(s["branch"], X)) < TOL, (key, b)
+    for b in range(len(specs)):
+        assert norm_rel(res[("1", "0")][0][b], res[("0", "0")][0][b]) < 1e-6, b
