@@ -534,8 +534,11 @@ def main():
                 (", network-joint sampler (per-step all-reduce)" if args.sampler == "network" else "") +
                 (", sequential Net::train sweep (one branch at a time)" if args.sampler == "sequential" else ""))
     wx_planes = path == "wide" and not args.hidden_bf16 and os.environ.get("BANN_WX_EXACT", "0") in ("", "0")
-    kernel_name = {"wide": "k_fused_grad_wx3" if wx_planes else "k_fused_grad_wx", "fused": "k_fused_grad_fx", "fused_large": "k_fused_grad_fxl",
-                   "layered": "k_gx_gemm"}[path]
+    # fxl shapes of 17..32 chunks run the head-wave kernel (kernels_fx.hip fxh_takes)
+    nch_b = -(-m_b // 64)
+    fxh = nch_b <= 32 and -(-nch_b // 4) >= 5 and os.environ.get("BANN_FXL_HEAD", "1") != "0"
+    kernel_name = {"wide": "k_fused_grad_wx3" if wx_planes else "k_fused_grad_wx", "fused": "k_fused_grad_fx",
+                   "fused_large": "k_fused_grad_fxh" if fxh else "k_fused_grad_fxl", "layered": "k_gx_gemm"}[path]
     # ---- kernel timing for the roofline: HIP events on the library stream around
     # the timed trajectory's own gradient launches (bann_set_launch_timing); the
     # back-to-back figure of the warmup session is reported beside it ----
