@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstring>
 #include <random>
 #include <string>
 #include <vector>
@@ -340,11 +341,15 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     p.d_gx = ctx->d_gen_scr;
     p.d_gxpre = ctx->d_gxpre_scr;
     p.d_fold = ctx->d_fold_scr;
-    if (!p.fold.empty())
-      CK(hipMemcpyAsync(p.d_fold, p.fold.data(), p.fold.size() * sizeof(FoldJob), hipMemcpyHostToDevice,
-                        ctx->stream));
     if ((int64_t)p.gx_pre.size() > ctx->gxpre_cap) return fail(ctx, BANN_E_STATE, "gx plan scratch overflow");
-    CK(hipMemcpyAsync(p.d_all, lists.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->plan_ev_pending) CK(hipEventSynchronize(ctx->ev_plan));  // the last plan's copy has read the stage
+    char* hs = ctx->h_plan_stage;
+    std::memcpy(hs, lists.data(), 2 * nb * sizeof(int32_t));
+    int64_t end = 2 * (int64_t)nb * (int64_t)sizeof(int32_t);
+    if (!p.fold.empty()) {
+      std::memcpy(hs + ctx->plan_off_fold, p.fold.data(), p.fold.size() * sizeof(FoldJob));
+      end = ctx->plan_off_fold + (int64_t)(p.fold.size() * sizeof(FoldJob));
+    }
     if (!p.gx.empty()) {
       CK(hipMemcpyAsync(p.d_gx, p.gx.data(), p.gx.size() * sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
       CK(hipMemcpyAsync(p.d_gxpre, p.gx_pre.data(), p.gx_pre.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -354,10 +359,14 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
     for (auto& g : p.groups) {
       if (off + (int64_t)g.items.size() > ctx->items_cap) return fail(ctx, BANN_E_STATE, "work-item scratch overflow");
       g.d_items = ctx->d_items_scr + off;
-      CK(hipMemcpyAsync(g.d_items, g.items.data(), g.items.size() * sizeof(GradItem), hipMemcpyHostToDevice,
-                        ctx->stream));
+      std::memcpy(hs + ctx->plan_off_items + off * (int64_t)sizeof(GradItem), g.items.data(),
+                  g.items.size() * sizeof(GradItem));
       off += (int64_t)g.items.size();
     }
+    if (off > 0) end = ctx->plan_off_items + off * (int64_t)sizeof(GradItem);
+    CK(hipMemcpyAsync(ctx->d_plan_scr, hs, (size_t)end, hipMemcpyHostToDevice, ctx->stream));
+    CK(hipEventRecord(ctx->ev_plan, ctx->stream));
+    ctx->plan_ev_pending = true;
   }
   return BANN_OK;
 }
@@ -496,7 +505,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_sigb, ctx->d_theta, ctx->d_mom, ctx->d_eps, ctx->d_theta0, ctx->d_lam, ctx->d_lamld,
                   ctx->d_grad, ctx->d_part, ctx->d_rss_part, ctx->d_y, ctx->d_pred, ctx->d_pred0, ctx->d_scr, ctx->d_eprec,
                   ctx->d_u, ctx->d_h0, ctx->d_htrace, ctx->d_ld, ctx->d_rss, ctx->d_status, ctx->d_uturn,
-                  ctx->d_list_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_fold_scr, ctx->d_items_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
+                  ctx->d_plan_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt,
                   ctx->d_res_part, ctx->d_ones, ctx->d_cm};
@@ -507,6 +516,16 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
   if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
   if (ctx->h_res_stat) (void)hipHostFree(ctx->h_res_stat);
+  if (ctx->plan_ev_pending && ctx->ev_plan) (void)hipEventSynchronize(ctx->ev_plan);
+  if (ctx->u_ev_pending && ctx->ev_u) (void)hipEventSynchronize(ctx->ev_u);
+  if (ctx->h_u_stage) (void)hipHostFree(ctx->h_u_stage);
+  if (ctx->ev_u) (void)hipEventDestroy(ctx->ev_u);
+  if (ctx->h_plan_stage) (void)hipHostFree(ctx->h_plan_stage);
+  if (ctx->ev_plan) (void)hipEventDestroy(ctx->ev_plan);
+  if (ctx->prec_ev_pending && ctx->ev_prec) (void)hipEventSynchronize(ctx->ev_prec);
+  if (ctx->h_prec_stage) (void)hipHostFree(ctx->h_prec_stage);
+  if (ctx->d_prec_stage) (void)hipFree(ctx->d_prec_stage);
+  if (ctx->ev_prec) (void)hipEventDestroy(ctx->ev_prec);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BANN_OK;
@@ -1024,13 +1043,23 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_rss, nb));
   CK(dalloc(&ctx->d_status, nb));
   CK(dalloc(&ctx->d_uturn, nb));
-  CK(dalloc(&ctx->d_list_scr, 2 * nb));
   CK(dalloc(&ctx->d_gen_scr, nb));
-  CK(dalloc(&ctx->d_fold_scr, nb));
   ctx->gxpre_cap = (int64_t)(3 * BANN_MAXL) * (n_gx + gx_ngroups + 2);
   CK(dalloc(&ctx->d_gxpre_scr, ctx->gxpre_cap));
-  CK(dalloc(&ctx->d_items_scr, items + ctx->solo_rss_cap));  // a solo plan has <= solo_rss_cap items
-  ctx->items_cap = items + ctx->solo_rss_cap;
+  ctx->items_cap = items + ctx->solo_rss_cap;  // a solo plan has <= solo_rss_cap items
+  {  // a per-call plan's branch lists, fold jobs and work items: one device block, filled by
+     // ONE copy from a pinned stage (build_plan; was three copies per bann_hmc_step call)
+    auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+    ctx->plan_off_fold = al(2 * (int64_t)nb * (int64_t)sizeof(int32_t));
+    ctx->plan_off_items = ctx->plan_off_fold + al((int64_t)nb * (int64_t)sizeof(FoldJob));
+    ctx->plan_scr_bytes = ctx->plan_off_items + ctx->items_cap * (int64_t)sizeof(GradItem);
+    CK(hipMalloc((void**)&ctx->d_plan_scr, (size_t)ctx->plan_scr_bytes));
+    CK(hipHostMalloc((void**)&ctx->h_plan_stage, (size_t)ctx->plan_scr_bytes, hipHostMallocDefault));
+    CK(hipEventCreateWithFlags(&ctx->ev_plan, hipEventDisableTiming));
+    ctx->d_list_scr = reinterpret_cast<int32_t*>(ctx->d_plan_scr);
+    ctx->d_fold_scr = reinterpret_cast<FoldJob*>(ctx->d_plan_scr + ctx->plan_off_fold);
+    ctx->d_items_scr = reinterpret_cast<GradItem*>(ctx->d_plan_scr + ctx->plan_off_items);
+  }
   // every branch's tile image in ONE batched pack launch (no per-branch sync), the
   // marker statistics in one gather, the precision-derived arrays in one copy each
   std::vector<int32_t> allidx;
@@ -1135,20 +1164,61 @@ extern "C" int bann_branch_get_params(bann_ctx* ctx, int32_t b, float* out) {
 
 // device copies derived from the host precision vector h.prec: per-parameter
 // prior multipliers, error precision, Izmailov step bases
+// the staged arrays of upload_precisions -> their device homes (one launch)
+__global__ void k_scatter_prec(const char* __restrict__ stage, int P, float* __restrict__ lam,
+                               float* __restrict__ lamld, double* __restrict__ sbase, float* __restrict__ ep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* sb = reinterpret_cast<const double*>(stage);
+  const float* l = reinterpret_cast<const float*>(stage + 8 * (size_t)P);
+  if (i < P) {
+    sbase[i] = sb[i];
+    lam[i] = l[i];
+    lamld[i] = l[P + i];
+  }
+  if (i == 0) *ep = l[2 * P];
+}
+
+// One branch's precision-derived device arrays (prior multipliers, error precision,
+// Izmailov step bases): staged in pinned memory as [sbase (f64) | lam | lamld | ep], one
+// H2D copy and one scatter launch, no host wait -- the sequential driver does this once
+// per branch update (it was four copies and a stream synchronisation).  The staging
+// buffer is reused after the previous upload's copy has completed (event).
 static int upload_precisions(bann_ctx* ctx, int32_t b) {
   const BranchHost& h = ctx->br[b];
   std::vector<float> lam, lamld;
   float ep = 1.f;
   expand_precisions(h, lam, lamld, ep);
-  CK(hipMemcpyAsync(ctx->d_lam + h.dev.p_off, lam.data(), h.P * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_lamld + h.dev.p_off, lamld.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
-                    ctx->stream));
-  CK(hipMemcpyAsync(ctx->d_eprec + b, &ep, sizeof(float), hipMemcpyHostToDevice, ctx->stream));
   std::vector<double> sbase;
   step_bases(h, sbase);
-  CK(hipMemcpyAsync(ctx->d_stepbase + h.dev.p_off, sbase.data(), h.P * sizeof(double), hipMemcpyHostToDevice,
-                    ctx->stream));
-  CK(hipStreamSynchronize(ctx->stream));
+  const size_t bytes = 16 * (size_t)h.P + 16;
+  if (bytes > ctx->prec_stage_cap) {
+    if (ctx->prec_ev_pending) CK(hipEventSynchronize(ctx->ev_prec));
+    if (ctx->h_prec_stage) (void)hipHostFree(ctx->h_prec_stage);
+    if (ctx->d_prec_stage) (void)hipFree(ctx->d_prec_stage);
+    ctx->h_prec_stage = nullptr;
+    ctx->d_prec_stage = nullptr;
+    ctx->prec_stage_cap = 0;
+    size_t cap = bytes;
+    for (const auto& o : ctx->br) cap = std::max(cap, 16 * (size_t)o.P + 16);
+    CK(hipHostMalloc((void**)&ctx->h_prec_stage, cap, hipHostMallocDefault));
+    CK(hipMalloc((void**)&ctx->d_prec_stage, cap));
+    if (!ctx->ev_prec) CK(hipEventCreateWithFlags(&ctx->ev_prec, hipEventDisableTiming));
+    ctx->prec_stage_cap = cap;
+    ctx->prec_ev_pending = false;
+  }
+  if (ctx->prec_ev_pending) CK(hipEventSynchronize(ctx->ev_prec));  // the last upload's copy has read the stage
+  char* st = ctx->h_prec_stage;
+  std::memcpy(st, sbase.data(), 8 * (size_t)h.P);
+  std::memcpy(st + 8 * (size_t)h.P, lam.data(), 4 * (size_t)h.P);
+  std::memcpy(st + 12 * (size_t)h.P, lamld.data(), 4 * (size_t)h.P);
+  std::memcpy(st + 16 * (size_t)h.P, &ep, sizeof(float));
+  CK(hipMemcpyAsync(ctx->d_prec_stage, st, bytes, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_scatter_prec, dim3((unsigned)((h.P + 255) / 256)), dim3(256), 0, ctx->stream, ctx->d_prec_stage,
+                     (int)h.P, ctx->d_lam + h.dev.p_off, ctx->d_lamld + h.dev.p_off, ctx->d_stepbase + h.dev.p_off,
+                     ctx->d_eprec + b);
+  CK(hipGetLastError());
+  CK(hipEventRecord(ctx->ev_prec, ctx->stream));
+  ctx->prec_ev_pending = true;
   return BANN_OK;
 }
 
@@ -1513,13 +1583,21 @@ int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t 
     CK(hipGetLastError());
   }
   bool host_data = momentum || (!device_eps);
-  if (u) {  // injected acceptance uniforms (parity runs)
-    std::vector<float> uu(ctx->br.size(), 0.f);
-    for (size_t i = 0; i < p.all.size(); ++i) uu[p.all[i]] = u[i];
-    CK(hipMemcpyAsync(ctx->d_u, uu.data(), uu.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    host_data = true;
+  if (u) {  // injected acceptance uniforms (parity runs; the sequential driver's host draws)
+    // staged in pinned memory that outlives the copy: no host wait here (the stage is
+    // reused once the previous call's copy has completed)
+    if (!ctx->h_u_stage) {
+      CK(hipHostMalloc((void**)&ctx->h_u_stage, ctx->br.size() * sizeof(float), hipHostMallocDefault));
+      CK(hipEventCreateWithFlags(&ctx->ev_u, hipEventDisableTiming));
+      std::fill(ctx->h_u_stage, ctx->h_u_stage + ctx->br.size(), 0.f);
+    }
+    if (ctx->u_ev_pending) CK(hipEventSynchronize(ctx->ev_u));
+    for (size_t i = 0; i < p.all.size(); ++i) ctx->h_u_stage[p.all[i]] = u[i];
+    CK(hipMemcpyAsync(ctx->d_u, ctx->h_u_stage, ctx->br.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    CK(hipEventRecord(ctx->ev_u, ctx->stream));
+    ctx->u_ev_pending = true;
     CK(hipMemsetAsync(ctx->d_htrace, 0xFF, ctx->br.size() * ctx->htrace_cap * sizeof(double), ctx->stream));
-    CK(hipStreamSynchronize(ctx->stream));  // uu goes out of scope
+    if (host_data) CK(hipStreamSynchronize(ctx->stream));  // host step sizes / momenta copied
     return BANN_OK;
   }
   // acceptance uniforms u ~ U(0,1) per branch (branch_sampler.rs:546-548) on the device

@@ -24,6 +24,10 @@
 
 #define BANN_NET_MAXL 64  // layer widths read back per branch (bann_branch_info)
 
+// bann_residual.hip (library-internal): bann_residual_from_target + bann_residual_shift(add) in one launch
+int residual_from_target_shift(bann_ctx* ctx, int32_t b, float add, double* sum, double* sumsq, double* sum_after,
+                               double* sumsq_after);
+
 namespace {
 
 enum { P_RIDGE_ARD = 0, P_RIDGE_BASE = 1, P_LASSO_ARD = 2, P_LASSO_BASE = 3, P_STD_NORMAL = 4 };
@@ -933,9 +937,11 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   if (status == BANN_ACCEPTED) ++t->nacc;
   if (status == BANN_REJECTED_EARLY) ++t->nearly;
   CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
-  // net.rs:292-300: residual = target - f_b(final) (accepted: y_pred; rejected: prev_pred)
-  double sr = 0.0;
-  CKB(bann_residual_from_target(t->ctx, b, &sr, &t->rss_cur));
+  // net.rs:292-300: residual = target - f_b(final) (accepted: y_pred; rejected: prev_pred),
+  // and the output-bias shift of net.rs:321 (residual += bias) in the same launch: nothing
+  // between the two touches the residual (sr_bias: its sum after the shift)
+  double sr = 0.0, sr_bias = 0.0;
+  CKB(residual_from_target_shift(t->ctx, b, t->ob_bias, &sr, &t->rss_cur, &sr_bias, nullptr));
   if (status == BANN_ACCEPTED) update_lpd(t, b, others);
   // to_cfg + GlobalParams::update_from_branch_cfg (net.rs:303-305, params.rs:41-56)
   B.ows_reg_sum = (float)(others + B.out_stat());
@@ -951,7 +957,7 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   }
   // output bias (net.rs:319-332): residual += bias, draw, residual -= bias
   t->ob_eprec = t->g_eprec;
-  CKB(bann_residual_shift(t->ctx, t->ob_bias, &sr, nullptr));
+  sr = sr_bias;  // residual += bias happened with the residual update above
   if (cfg->sampled_output_bias) {
     // sample_prior_precision passes the prior SHAPE as the scale (net.rs:61-66)
     const double bsq = (double)t->ob_bias * t->ob_bias;

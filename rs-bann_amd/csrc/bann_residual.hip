@@ -21,8 +21,8 @@
 // out[b][i] = r[i] + pred[b][i] for every listed branch (net.rs:279-280: the
 // branch is fitted to the residual plus its own prediction)
 __global__ void __launch_bounds__(RES_BLK) k_targets_from_residual(DevState st, const int32_t* __restrict__ blist,
-                                                                   const float* __restrict__ r) {
-  const int b = blist[blockIdx.y];
+                                                                   int b1, const float* __restrict__ r) {
+  const int b = blist ? blist[blockIdx.y] : b1;  // one branch: by value (no list upload, no host wait)
   const int64_t i = ((int64_t)blockIdx.x * RES_BLK + threadIdx.x) * 4;
   const int64_t o = (int64_t)b * st.n + i;
   if (i + 4 <= st.n && (st.n & 3) == 0) {
@@ -40,12 +40,22 @@ __global__ void __launch_bounds__(RES_BLK) k_targets_from_residual(DevState st, 
 //                                             final prediction; a rejected branch's pred is f(theta_0))
 //   op 2: r = (y - add) - sum_b pred_b        (initialize_stats, net.rs:158-171, branches in order)
 //   op 3: r unchanged (statistics only)
+//   op 4: r = (y_b - pred_b) + add            (op 1 then op 0 in one pass: the sequential
+//                                             driver's residual update and output-bias shift;
+//                                             the statistics of both states, four values)
+// The statistics come out of the same launch: every block writes its (sum, sum of
+// squares) partial, the last block to arrive (an agent-scope counter, reset by it)
+// adds the partials in block order -- the order of the former second launch,
+// k_residual_stats -- and writes the pair to out (device) and out_host (the mapped
+// pinned result the host reads after the stream synchronises: no copy launch).
 __global__ void __launch_bounds__(RES_BLK) k_residual_op(DevState st, float* __restrict__ r, int op, int b,
                                                          const float* __restrict__ y, float add,
                                                          const int32_t* __restrict__ blist, int nb,
-                                                         double* __restrict__ part) {
-  __shared__ double s_s[RES_BLK / 64], s_q[RES_BLK / 64];
-  double s = 0.0, q = 0.0;
+                                                         double* __restrict__ part, unsigned* __restrict__ cnt,
+                                                         double* __restrict__ out, double* __restrict__ out_host) {
+  __shared__ double s_s[RES_BLK / 64], s_q[RES_BLK / 64], s_s2[RES_BLK / 64], s_q2[RES_BLK / 64];
+  __shared__ int s_last;
+  double s = 0.0, q = 0.0, s2 = 0.0, q2 = 0.0;
   const int64_t base = (int64_t)blockIdx.x * RES_BLK * RES_PER + threadIdx.x;
 #pragma unroll
   for (int k = 0; k < RES_PER; ++k) {
@@ -54,7 +64,7 @@ __global__ void __launch_bounds__(RES_BLK) k_residual_op(DevState st, float* __r
     float v;
     if (op == 0) {
       v = r[i] + add;
-    } else if (op == 1) {
+    } else if (op == 1 || op == 4) {
       const int64_t o = (int64_t)b * st.n + i;
       v = st.y[o] - st.pred[o];
     } else if (op == 2) {
@@ -63,47 +73,79 @@ __global__ void __launch_bounds__(RES_BLK) k_residual_op(DevState st, float* __r
     } else {
       v = r[i];
     }
-    if (op != 3) r[i] = v;
     s += (double)v;
     q += (double)v * (double)v;
+    if (op == 4) {
+      v = v + add;
+      s2 += (double)v;
+      q2 += (double)v * (double)v;
+    }
+    if (op != 3) r[i] = v;
   }
+  const int NV = op == 4 ? 4 : 2;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o);
     q += __shfl_xor(q, o);
+    s2 += __shfl_xor(s2, o);
+    q2 += __shfl_xor(q2, o);
   }
   if ((threadIdx.x & 63) == 0) {
     s_s[threadIdx.x >> 6] = s;
     s_q[threadIdx.x >> 6] = q;
+    s_s2[threadIdx.x >> 6] = s2;
+    s_q2[threadIdx.x >> 6] = q2;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double ts = 0.0, tq = 0.0;
+    double ts = 0.0, tq = 0.0, ts2 = 0.0, tq2 = 0.0;
     for (int w = 0; w < RES_BLK / 64; ++w) {
       ts += s_s[w];
       tq += s_q[w];
+      ts2 += s_s2[w];
+      tq2 += s_q2[w];
     }
-    part[2 * blockIdx.x] = ts;
-    part[2 * blockIdx.x + 1] = tq;
+    part[NV * blockIdx.x] = ts;
+    part[NV * blockIdx.x + 1] = tq;
+    if (NV == 4) {
+      part[NV * blockIdx.x + 2] = ts2;
+      part[NV * blockIdx.x + 3] = tq2;
+    }
+    __threadfence();  // release the partial before counting in
+    s_last = atomicAdd(cnt, 1u) == gridDim.x - 1;
   }
-}
-
-// fixed-order sum of the block partials -> out[0] = sum, out[1] = sum of squares
-__global__ void __launch_bounds__(64) k_residual_stats(const double* __restrict__ part, int nblk,
-                                                       double* __restrict__ out) {
-  double s = 0.0, q = 0.0;
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  __threadfence();  // acquire every block's partial
+  const int nblk = (int)gridDim.x;
+  double ts = 0.0, tq = 0.0, ts2 = 0.0, tq2 = 0.0;
   for (int k = threadIdx.x; k < nblk; k += 64) {
-    s += part[2 * k];
-    q += part[2 * k + 1];
+    ts += part[NV * k];
+    tq += part[NV * k + 1];
+    if (NV == 4) {
+      ts2 += part[NV * k + 2];
+      tq2 += part[NV * k + 3];
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o);
-    q += __shfl_xor(q, o);
+    ts += __shfl_xor(ts, o);
+    tq += __shfl_xor(tq, o);
+    ts2 += __shfl_xor(ts2, o);
+    tq2 += __shfl_xor(tq2, o);
   }
   if (threadIdx.x == 0) {
-    out[0] = s;
-    out[1] = q;
+    out[0] = ts;
+    out[1] = tq;
+    out[2] = ts2;
+    out[3] = tq2;
+    if (out_host) {
+      out_host[0] = ts;
+      out_host[1] = tq;
+      out_host[2] = ts2;
+      out_host[3] = tq2;
+    }
+    *cnt = 0u;  // the next launch counts from zero (stream order)
   }
 }
 
@@ -125,8 +167,11 @@ static int ensure_residual(bann_ctx* ctx) {
   if (!ctx->d_res) {
     CK(dalloc(&ctx->d_res, ctx->n));
     CK(hipMemsetAsync(ctx->d_res, 0, ctx->n * sizeof(float), ctx->stream));
-    CK(dalloc(&ctx->d_res_part, 2 * res_blocks(ctx->n) + 2));
-    CK(hipHostMalloc((void**)&ctx->h_res_stat, 2 * sizeof(double), hipHostMallocDefault));
+    // block partials (up to four per block), the result (four), the counter
+    CK(dalloc(&ctx->d_res_part, 4 * res_blocks(ctx->n) + 8));
+    CK(hipMemsetAsync(ctx->d_res_part, 0, (4 * res_blocks(ctx->n) + 8) * sizeof(double), ctx->stream));
+    CK(hipHostMalloc((void**)&ctx->h_res_stat, 4 * sizeof(double), hipHostMallocDefault));
+    CK(hipHostGetDevicePointer((void**)&ctx->d_res_stat_host, ctx->h_res_stat, 0));
   }
   return BANN_OK;
 }
@@ -145,19 +190,22 @@ int ensure_predictions(bann_ctx* ctx, const int32_t* branches, int32_t nb) {
 }
 
 static int residual_op(bann_ctx* ctx, int op, int b, const float* d_y, float add, const int32_t* d_list, int nb,
-                       double* sum, double* sumsq) {
+                       double* sum, double* sumsq, double* after = nullptr) {
   const int64_t nblk = res_blocks(ctx->n);
+  const bool want = sum || sumsq || after;
   hipLaunchKernelGGL(k_residual_op, dim3((unsigned)nblk), dim3(RES_BLK), 0, ctx->stream, ctx->st, ctx->d_res, op, b,
-                     d_y, add, d_list, nb, ctx->d_res_part);
-  hipLaunchKernelGGL(k_residual_stats, dim3(1), dim3(64), 0, ctx->stream, ctx->d_res_part, (int)nblk,
-                     ctx->d_res_part + 2 * nblk);
+                     d_y, add, d_list, nb, ctx->d_res_part,
+                     reinterpret_cast<unsigned*>(ctx->d_res_part + 4 * nblk + 4), ctx->d_res_part + 4 * nblk,
+                     want ? ctx->d_res_stat_host : nullptr);
   CK(hipGetLastError());
-  if (sum || sumsq) {
-    CK(hipMemcpyAsync(ctx->h_res_stat, ctx->d_res_part + 2 * nblk, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                      ctx->stream));
+  if (want) {
     CK(hipStreamSynchronize(ctx->stream));
     if (sum) *sum = ctx->h_res_stat[0];
     if (sumsq) *sumsq = ctx->h_res_stat[1];
+    if (after) {
+      after[0] = ctx->h_res_stat[2];
+      after[1] = ctx->h_res_stat[3];
+    }
   }
   return BANN_OK;
 }
@@ -237,6 +285,12 @@ extern "C" int bann_rebuild_targets(bann_ctx* ctx, const int32_t* branches, int3
   if (rc) return rc;
   // the branch list: the leapfrog session's persistent list when it is the same set
   const int32_t* d_list = nullptr;
+  if (nb == 1) {  // one branch (the sequential driver): by value
+    hipLaunchKernelGGL(k_targets_from_residual, dim3((unsigned)((ctx->n + 4 * RES_BLK - 1) / (4 * RES_BLK)), 1u),
+                       dim3(RES_BLK), 0, ctx->stream, ctx->st, nullptr, branches[0], r);
+    CK(hipGetLastError());
+    return BANN_OK;
+  }
   if (ctx->lf.owns && ctx->lf.all.size() == (size_t)nb && std::equal(branches, branches + nb, ctx->lf.all.begin())) {
     d_list = ctx->lf.d_all;
   } else {
@@ -244,7 +298,7 @@ extern "C" int bann_rebuild_targets(bann_ctx* ctx, const int32_t* branches, int3
     d_list = ctx->d_list_scr;
   }
   hipLaunchKernelGGL(k_targets_from_residual, dim3((unsigned)((ctx->n + 4 * RES_BLK - 1) / (4 * RES_BLK)), (unsigned)nb),
-                     dim3(RES_BLK), 0, ctx->stream, ctx->st, d_list, r);
+                     dim3(RES_BLK), 0, ctx->stream, ctx->st, d_list, 0, r);
   CK(hipGetLastError());
   if (d_list == ctx->d_list_scr) CK(hipStreamSynchronize(ctx->stream));  // host list copied
   return BANN_OK;
@@ -260,4 +314,24 @@ extern "C" int bann_residual_from_target(bann_ctx* ctx, int32_t b, double* sum, 
   rc = ensure_predictions(ctx, &b, 1);
   if (rc) return rc;
   return residual_op(ctx, 1, b, nullptr, 0.f, nullptr, 0, sum, sumsq);
+}
+
+// the sequential driver's residual update (net.rs:292-300) and the output-bias shift that
+// follows it (net.rs:319-321) in one launch: residual = (y_b - f_b) + add; stats of the
+// residual before (sum, sum of squares) and after the shift -- the bits of
+// bann_residual_from_target followed by bann_residual_shift(add)
+int residual_from_target_shift(bann_ctx* ctx, int32_t b, float add, double* sum, double* sumsq, double* sum_after,
+                               double* sumsq_after) {
+  int rc = ensure_residual(ctx);
+  if (rc) return rc;
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  if (!session_free(ctx)) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  rc = ensure_predictions(ctx, &b, 1);
+  if (rc) return rc;
+  double aft[2] = {0.0, 0.0};
+  rc = residual_op(ctx, 4, b, nullptr, add, nullptr, 0, sum, sumsq, aft);
+  if (rc) return rc;
+  if (sum_after) *sum_after = aft[0];
+  if (sumsq_after) *sumsq_after = aft[1];
+  return BANN_OK;
 }

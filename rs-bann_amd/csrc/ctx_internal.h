@@ -151,6 +151,20 @@ struct bann_ctx {
   float* d_res = nullptr;
   double* d_res_part = nullptr;
   double* h_res_stat = nullptr;
+  double* d_res_stat_host = nullptr;  // the same pinned pair, as the kernels address it
+  char* h_prec_stage = nullptr;  // upload_precisions: pinned staging of one branch's precision arrays
+  char* d_prec_stage = nullptr;
+  size_t prec_stage_cap = 0;
+  hipEvent_t ev_prec = nullptr;  // the staging copy of the last upload
+  bool prec_ev_pending = false;
+  char* d_plan_scr = nullptr;    // one block: d_list_scr | d_fold_scr | d_items_scr (build_plan)
+  char* h_plan_stage = nullptr;  // its pinned stage (one copy per per-call plan)
+  int64_t plan_scr_bytes = 0, plan_off_fold = 0, plan_off_items = 0;
+  hipEvent_t ev_plan = nullptr;
+  bool plan_ev_pending = false;
+  float* h_u_stage = nullptr;    // traj_prepare: injected acceptance uniforms, pinned
+  hipEvent_t ev_u = nullptr;
+  bool u_ev_pending = false;
   // pred_ok[b]: the prediction row of branch b is f_b(theta_b) at the current parameters
   std::vector<char> pred_ok;
   // in-trajectory launch timing (bann_set_launch_timing): HIP events around every

@@ -226,48 +226,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   const int64_t n = st.n;
   const int tb = it.frag_begin >> 2, te = (it.frag_end + 3) >> 2;
 
-  // ---- branch constants: head weights (LDS, then scalar registers), W0 digits, column scale ----
-  const float* th = st.theta + bd.p_off;
-  for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
-    const int l = t / 20, r = t - l * 20;
-    float v = 0.f;
-    if (r < 16) {  // Wh[l][j][k] = W_l[j][k] (l >= 1), zero padded to 4 x 4
-      const int j = r >> 2, k = r & 3;
-      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
-    } else {  // bias[0] = c0 (folded standardisation), bias[l] = b_l
-      const int k = r - 16;
-      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
-      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
-    }
-    s_hw[l][r] = v;
-  }
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
-  float zscale = st.fc[b].scale[g];
-  for (int c = wave; c < nch; c += NW)  // W0 digit image -> LDS (shared by the four waves)
-    *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
-        *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
-  // retire the prologue loads and hide their provenance: inside the tile loop the
-  // only vector-memory waits are the explicit, counted ones on this wave's DMAs
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("" : "+v"(zscale));
-  __syncthreads();
-  v4i rowsum64 = v4i{0, 0, 0, 0};  // the forward's facc[3] start (field 3 stored as code - 1)
-  for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
-  // head weights as wave-uniform values: scalar registers for the whole item (the
-  // per-tile LDS broadcasts serialised the head on their latencies)
-  float uW[NL][4][4], uB[NH][4];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        uW[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l][4 * j + k]) : 0.f;
-    if (l < NH)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l][16 + k]);
-  }
-
   // ---- per-lane LDS offsets ----
   const int gsw = g & 1;
   const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
@@ -312,6 +271,59 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     const int64_t row = 64 * (int64_t)tt + iota;
     glds4(ybr + (row < n ? row : n - 1), &s_y[wave][sl][0]);
   };
+  // the item's first two tiles are issued before the prologue's loads, so their HBM latency
+  // overlaps the W0-digit and head-weight loads (a solo item -- the sequential driver's
+  // one-branch steps -- has one tile per wave: the launch was that latency longer)
+  int tt = tb + wave, sl = 0;
+  if (tt < te) {
+    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
+    issue_y(tt, 0);
+    if (tt + NW < te) {
+      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
+      issue_y(tt + NW, 1);
+    }
+  }
+  // ---- branch constants: head weights (LDS, then scalar registers), W0 digits, column scale ----
+  const float* th = st.theta + bd.p_off;
+  for (int t = threadIdx.x; t < NL * 20; t += 64 * NW) {
+    const int l = t / 20, r = t - l * 20;
+    float v = 0.f;
+    if (r < 16) {  // Wh[l][j][k] = W_l[j][k] (l >= 1), zero padded to 4 x 4
+      const int j = r >> 2, k = r & 3;
+      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+    } else {  // bias[0] = c0 (folded standardisation), bias[l] = b_l
+      const int k = r - 16;
+      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+    }
+    s_hw[l][r] = v;
+  }
+  float zscale = st.fc[b].scale[g];
+  for (int c = wave; c < nch; c += NW)  // W0 digit image -> LDS (shared by the four waves)
+    *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
+        *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+  // retire the prologue loads and hide their provenance: inside the tile loop the
+  // only vector-memory waits are the explicit, counted ones on this wave's DMAs
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(zscale));
+  __syncthreads();
+  v4i rowsum64 = v4i{0, 0, 0, 0};  // the forward's facc[3] start (field 3 stored as code - 1)
+  for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
+  // head weights as wave-uniform values: scalar registers for the whole item (the
+  // per-tile LDS broadcasts serialised the head on their latencies)
+  float uW[NL][4][4], uB[NH][4];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        uW[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[l][4 * j + k]) : 0.f;
+    if (l < NH)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l][16 + k]);
+  }
+
 
   // ---- accumulators ----
   v4i acc[32];  // dW0 digit sums per 16-marker window u (lane: column g, marker 16u + i16)
@@ -338,15 +350,6 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime(), mt0 = __builtin_amdgcn_s_memtime();
   unsigned long long t_last = mt0;
 #endif
-  int tt = tb + wave, sl = 0;
-  if (tt < te) {
-    for (int c = 0; c < nch; ++c) issue_chunk(tt, 0, c);
-    issue_y(tt, 0);
-    if (tt + NW < te) {
-      for (int c = 0; c < nch; ++c) issue_chunk(tt + NW, 1, c);
-      issue_y(tt + NW, 1);
-    }
-  }
   for (; tt < te; tt += NW, sl ^= 1) {
     const bool more = tt + NW < te;
     const bool more2 = tt + 2 * NW < te;  // tile tt + 2 NW goes into this slot
@@ -746,12 +749,25 @@ static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nite
 // full8: every branch of this launch group has exactly 8 chunks; upd_cnt != null:
 // the fused leapfrog update in the launch's tail (mode upd_mode, step upd_step),
 // folds != null: a solo plan's fold jobs, run by the tail before the update
+template <int NL>
+static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
+                          int slot_kib, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt,
                           const FoldJob* folds, hipStream_t s) {
   if (nitems <= 0) return;
   const int wp = write_pred, um = upd_mode, us = upd_step;
   const FoldJob* fo = upd_cnt ? folds : nullptr;
+  {  // BANN_FX_HEAD=1 (experiment): 8-chunk branches on the head-wave kernel -- two compute
+     // waves of four chunks and one head wave per tile, four workgroups per CU
+    const char* e = getenv("BANN_FX_HEAD");
+    if (e && atoi(e) != 0 && full8 && upd_cnt == nullptr && L >= 2 && L <= 4) {
+      if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, 2, wp, 4, s);
+      if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, 2, wp, 4, s);
+      if (L == 4) launch_fxh_nl<4>(st, items, nitems, act, 2, wp, 4, s);
+      return;
+    }
+  }
   switch (L * 2 + (full8 ? 1 : 0)) {
     case 4: launch_fx_nl<2, 0>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
     case 5: launch_fx_nl<2, 8>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
@@ -1478,15 +1494,15 @@ int fxl_cpw(int nchunks) {
 bool fxh_takes(int nw, int cpw);
 template <int NL>
 static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
-                          hipStream_t s);
+                          int slot_kib, hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                            int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s) {
   if (nitems <= 0 || nw < 1 || nw > FXL_MAXW || (cpw != 4 && cpw != 8)) return;
   if (fxh_takes(nw, cpw) && L >= 2 && L <= 4) {  // the head-wave kernel: ceil(4 nw / 5) compute waves
     const int nc = (4 * nw + FXH_CPW - 1) / FXH_CPW;
-    if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, nc, write_pred, s);
-    if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, nc, write_pred, s);
-    if (L == 4) launch_fxh_nl<4>(st, items, nitems, act, nc, write_pred, s);
+    if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, nc, write_pred, FXH_CPW, s);
+    if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, nc, write_pred, FXH_CPW, s);
+    if (L == 4) launch_fxh_nl<4>(st, items, nitems, act, nc, write_pred, FXH_CPW, s);
     return;
   }
   switch (L * 4 + (full ? 2 : 0) + (cpw == 4 ? 1 : 0)) {
@@ -1534,18 +1550,20 @@ void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t ni
 // from fxl only through the partition of the chunks over waves.
 // ===========================================================================
 
-int fxh_lds_bytes(int nc, int nl) {
+// slot_kib: the largest chunk count of a compute wave (one KiB per chunk and slot)
+int fxh_lds_bytes(int nc, int nl, int slot_kib) {
   const int ns = 8 + (nl - 2) * 20;
-  return nc * FXH_NSL * FXH_CPW * 1024 + 2 * nc * 64 * 16 + 2 * 4 * FX_DROW + 3 * 64 * 4 + 16 * 4 + nl * 20 * 4 +
+  return nc * FXH_NSL * slot_kib * 1024 + 2 * nc * 64 * 16 + 2 * 4 * FX_DROW + 3 * 64 * 4 + 16 * 4 + nl * 20 * 4 +
          ns * 4 + 4 * 4;
 }
 
 template <int NL, int ACT>
 __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
-    k_fused_grad_fxh(DevState st, const GradItem* __restrict__ items, int write_pred) {
+    k_fused_grad_fxh(DevState st, const GradItem* __restrict__ items, int write_pred, int slot_kib) {
   constexpr int NH = NL - 1;
   constexpr int NS = 8 + (NH - 1) * 20;
-  constexpr int CPW = FXH_CPW, SLOT = CPW * 1024, NSL = FXH_NSL;
+  constexpr int NSL = FXH_NSL;
+  const int SLOT = __builtin_amdgcn_readfirstlane(slot_kib) * 1024;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int NC = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6) - 1);
   char* const s_x = lds;                                                // [NC][NSL][SLOT]
@@ -1599,7 +1617,9 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
         for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[l * 20 + 16 + k]);
     }
     const int iota = 4 * i16 + g;
-    const float* ybr = st.y + bd.y_off;
+    // the tile's targets -- or, in network mode, the network's output error (as fx)
+    const bool net_err = st.nete != nullptr;
+    const float* ybr = net_err ? st.nete : st.y + bd.y_off;
     float* predb = st.pred + bd.y_off;
     auto issue_y = [&](int k) {
       const int64_t row = 64 * (int64_t)(tb + k) + iota;
@@ -1629,12 +1649,12 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
         // y(k) has landed: younger are store(k - 2), y(k + 1), store(k - 1)
         vm_wait_n(wp * (k >= 2) + (k + 1 < T) + wp * (k >= 1));
         __builtin_amdgcn_s_setprio(1);
-        // the NC partials in compute-wave order; all FXH_MAXC slots read (past NC they are
-        // other LDS bytes, not added), so the loads issue together
+        // the NC partials in compute-wave order; FXH_MAXC loads issued together (past NC
+        // they re-read the last partial, not added)
         const v4f* xz = s_zx + (k & 1) * NC * 64 + lane;
         v4f zp[FXH_MAXC];
 #pragma unroll
-        for (int w = 0; w < FXH_MAXC; ++w) zp[w] = xz[w * 64];
+        for (int w = 0; w < FXH_MAXC; ++w) zp[w] = xz[(w < NC ? w : NC - 1) * 64];
         v4f zs = zp[0];
 #pragma unroll
         for (int w = 1; w < FXH_MAXC; ++w)
@@ -1671,7 +1691,7 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
           float out = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) out = fmaf(a[NH - 1][j], uW[NL - 1][j][0], out);
-          const float e = valid ? out - yv : 0.f;
+          const float e = valid ? (net_err ? yv : out - yv) : 0.f;
           rss += (double)e * (double)e;
           float err[4];
 #pragma unroll
@@ -1927,18 +1947,18 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
 
 template <int NL>
 static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
-                          hipStream_t s) {
+                          int slot_kib, hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * (nc + 1));
-  const size_t shm = (size_t)fxh_lds_bytes(nc, NL);
+  const size_t shm = (size_t)fxh_lds_bytes(nc, NL, slot_kib);
 #define FXH_GO(A)                                                                                       \
   do {                                                                                                  \
     static bool attr_ = false;                                                                          \
     if (!attr_) {                                                                                       \
       (void)hipFuncSetAttribute((const void*)k_fused_grad_fxh<NL, A>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                fxh_lds_bytes(FXH_MAXC, 4));                                            \
+                                fxh_lds_bytes(FXH_MAXC, 4, FXH_CPW));                                   \
       attr_ = true;                                                                                     \
     }                                                                                                   \
-    hipLaunchKernelGGL((k_fused_grad_fxh<NL, A>), grid, block, shm, s, st, items, wp);                  \
+    hipLaunchKernelGGL((k_fused_grad_fxh<NL, A>), grid, block, shm, s, st, items, wp, slot_kib);        \
   } while (0)
   switch (act) {
     case 0: FXH_GO(0); break;
