@@ -749,25 +749,12 @@ static void launch_fx_nl(const DevState& st, const GradItem* items, int32_t nite
 // full8: every branch of this launch group has exactly 8 chunks; upd_cnt != null:
 // the fused leapfrog update in the launch's tail (mode upd_mode, step upd_step),
 // folds != null: a solo plan's fold jobs, run by the tail before the update
-template <int NL>
-static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
-                          int slot_kib, hipStream_t s);
 void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
                           int full8, int write_pred, int upd_mode, int upd_step, int32_t* upd_cnt,
                           const FoldJob* folds, hipStream_t s) {
   if (nitems <= 0) return;
   const int wp = write_pred, um = upd_mode, us = upd_step;
   const FoldJob* fo = upd_cnt ? folds : nullptr;
-  {  // BANN_FX_HEAD=1 (experiment): 8-chunk branches on the head-wave kernel -- two compute
-     // waves of four chunks and one head wave per tile, four workgroups per CU
-    const char* e = getenv("BANN_FX_HEAD");
-    if (e && atoi(e) != 0 && full8 && upd_cnt == nullptr && L >= 2 && L <= 4) {
-      if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, 2, wp, 4, s);
-      if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, 2, wp, 4, s);
-      if (L == 4) launch_fxh_nl<4>(st, items, nitems, act, 2, wp, 4, s);
-      return;
-    }
-  }
   switch (L * 2 + (full8 ? 1 : 0)) {
     case 4: launch_fx_nl<2, 0>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
     case 5: launch_fx_nl<2, 8>(st, items, nitems, act, wp, um, us, upd_cnt, fo, s); break;
