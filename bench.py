@@ -506,8 +506,8 @@ def main():
     if timing:
         ctx.set_launch_timing(False)
         grad_ms, upd_ms, n_launch = ctx.launch_timing(reset=True)
-        if args.sampler == "network":
-            ctx.network_timing(reset=True)
+        if args.sampler == "network":   # the timed trajectory's forward-only launches and all-reduces
+            net_fwd_ms, net_ar_ms, net_n_ar = ctx.network_timing(reset=True)
     else:
         grad_ms, upd_ms, n_launch = b2b_grad_ms, b2b_upd_ms, 0
     if dist is not None:
@@ -648,6 +648,10 @@ def main():
             "setup_s": setup_s,
         }
         if args.sampler == "network":
+            if timing:
+                out["network_timing"] = {"forward_ms": net_fwd_ms, "allreduce_us_per_step": 1e3 * net_ar_ms,
+                                         "allreduces": net_n_ar,
+                                         "source": "HIP events around the timed trajectory's launches"}
             rule = ctx.network_step_rule_info()
             out["network_step_rule"] = {"kind": args.network_step_rule, "tau": args.network_tau,
                                         "fraction_scaled": rule["fraction_scaled"],

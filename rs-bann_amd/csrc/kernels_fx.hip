@@ -778,7 +778,8 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 // the counted wait at the top never waits on a piece younger than the tile).
 // ===========================================================================
 #ifndef FWD_NS
-#define FWD_NS 4  // tile slots per wave: the stream runs FWD_NS tiles ahead (4: one workgroup per CU)
+#define FWD_NS 2  // tile slots per wave: the stream runs FWD_NS tiles ahead (2: two workgroups per CU;
+                  // round 5, network line A/B: 379.6 / 381.2 vs 376.0 / 377.2 steps/s with 4, 376.6 / 378.2 with 3)
 #endif
 // all but the youngest k (0 .. 31) vector-memory operations of this wave are complete
 __device__ __forceinline__ void vm_wait_n(int k) {
