@@ -269,9 +269,10 @@ def main():
                     help="skip the untimed network-joint trajectory through the library's RCCL communicator "
                          "(a 1-rank one at N = 1) that runs before the warmup and is reported in the line "
                          "(network_check)")
-    ap.add_argument("--network-step-rule", default="common_mode", choices=["common_mode", "off"],
-                    help="network-joint step sizes: the common-mode water-filling rule (bann_set_network_step_rule, "
-                         "default) or the per-branch Izmailov steps as they are")
+    ap.add_argument("--network-step-rule", default="common_mode", choices=["common_mode", "adaptive", "off"],
+                    help="network-joint step sizes: the common-mode water-filling rule (bann_set_network_step_rule; "
+                         "default: adapted during the warmup, frozen for the timed and acceptance trajectories), "
+                         "adaptive (re-adapted before every trajectory) or the per-branch Izmailov steps as they are")
     ap.add_argument("--network-tau", type=float, default=1.0,
                     help="common-mode rule: omega eps of the network's common mode after the rule")
     ap.add_argument("--accept-trajectories", type=int, default=None,
@@ -326,7 +327,7 @@ def main():
     for k in range(nb):
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
-    ctx.set_network_step_rule(args.network_step_rule == "common_mode", args.network_tau)
+    ctx.set_network_step_rule(args.network_step_rule != "off", args.network_tau)
     path = ctx.kernel_path(0)
     assert path == ("layered" if heavy else "wide" if widths[0] > 4 else "fused" if m_b <= 512 else "fused_large")
     assert all(ctx.kernel_path(k) == path for k in range(nb))
@@ -486,6 +487,11 @@ def main():
         b2b_grad_ms, b2b_upd_ms = b2b_session(restore=True)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
+    if args.sampler == "network" and args.network_step_rule == "common_mode":
+        # the rule adapted its step factors during the warmup (burn-in); the timed and the
+        # acceptance trajectories sample with them frozen: step sizes independent of each
+        # trajectory's start, as HMC's reversibility asks (bann_set_network_step_rule)
+        ctx.set_network_step_rule("frozen", args.network_tau)
     if args.sampler == "branch":
         b2b_grad_ms, b2b_upd_ms = b2b_session(restore=False)
     timing = args.sampler in ("branch", "network") and not args.no_launch_timing

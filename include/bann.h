@@ -412,7 +412,11 @@ int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambd
  * eps_p min(1, t / (eps_p |g_p|)) with the largest t (within 2^(1/4)) such that
  * lambda_e / n sum_p min(eps_p |g_p|, t)^2 <= tau^2: the common mode runs at
  * omega eps <= tau while the parameters that do not drive it keep their steps.
- * Summed over the ranks (collective); not applied to injected step sizes. */
+ * Summed over the ranks (collective); not applied to injected step sizes.
+ * common_mode = 2 (frozen): the factors of the last adapted trajectory are applied
+ * again without recomputing g -- step sizes that do not depend on the trajectory's
+ * start, as HMC's reversibility asks; the sampler adapts during burn-in (1) and
+ * samples frozen (2), as bench.py does.  0 = off. */
 int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau);
 /* the last network trajectory's rule: [threshold t (inf: no step changed),
  * (omega eps)^2 of the common mode before (inf when some single parameter alone

@@ -436,10 +436,13 @@ class BannContext:
             C.byref(rss)))
         return dict(status=st.value, trace=tr, rss=rss.value)
 
-    def set_network_step_rule(self, common_mode: bool = True, tau: float = 1.0):
+    def set_network_step_rule(self, common_mode=True, tau: float = 1.0):
         """the network-joint state's step sizes (bann_set_network_step_rule): the common-mode
-        water-filling rule at omega eps <= tau (default on), or the per-branch steps as given."""
-        self._check(self._lib.bann_set_network_step_rule(self._h, int(common_mode), float(tau)))
+        water-filling rule at omega eps <= tau adapted before every trajectory (True / 1,
+        the default), frozen at the last adapted factors ("frozen" / 2: state-independent
+        steps for sampling after burn-in), or the per-branch steps as given (False / 0)."""
+        mode = 2 if common_mode == "frozen" else int(common_mode)
+        self._check(self._lib.bann_set_network_step_rule(self._h, mode, float(tau)))
 
     def network_step_rule_info(self) -> dict:
         """the last network trajectory's rule: threshold t, (omega eps)^2 of the common mode

@@ -508,7 +508,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_plan_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt,
-                  ctx->d_res_part, ctx->d_ones, ctx->d_cm};
+                  ctx->d_res_part, ctx->d_ones, ctx->d_cm, ctx->d_cm_scale};
   for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
   clear_graphs(ctx);
   comm_destroy(ctx);

@@ -187,8 +187,10 @@ extern "C" int bann_exchange_residual_device(bann_ctx* ctx) {
 
 extern "C" int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau) {
   if (!ctx) return BANN_E_ARG;
+  if (common_mode < 0 || common_mode > 2) return fail(ctx, BANN_E_ARG, "common_mode: 0 off, 1 adapt, 2 frozen");
   if (common_mode && !(tau > 0.f)) return fail(ctx, BANN_E_ARG, "tau must be positive");
-  ctx->cm_rule = common_mode != 0;
+  if (common_mode == 1 && ctx->cm_tau != tau) ctx->cm_have_scale = false;
+  ctx->cm_rule = common_mode;
   ctx->cm_tau = tau;
   return BANN_OK;
 }
@@ -207,6 +209,15 @@ namespace {
 int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e) {
   const int64_t n = ctx->n;
   const int32_t nb = (int32_t)p.all.size();
+  if (!ctx->d_cm_scale) {
+    const BranchHost& last = ctx->br.back();
+    CK(dalloc(&ctx->d_cm_scale, last.dev.p_off + last.P));
+  }
+  if (ctx->cm_rule == 2 && ctx->cm_have_scale) {  // frozen: the adapted factors, no gradient launch
+    launch_cm_rescale(ctx->st, p.d_all, nb, p.max_p, ctx->d_cm_scale, ctx->stream);
+    CK(hipGetLastError());
+    return BANN_OK;
+  }
   if (!ctx->d_ones) {
     CK(dalloc(&ctx->d_ones, n));
     std::vector<float> one((size_t)n, 1.f);
@@ -252,6 +263,9 @@ int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e
     }
   }
   if (kst < 0) {  // the common mode is already below tau: steps unchanged
+    launch_cm_apply(ctx->st, p.d_all, nb, p.max_p, INFINITY, ctx->d_cm_scale, ctx->stream);  // factors 1
+    CK(hipGetLastError());
+    ctx->cm_have_scale = true;
     ctx->cm_info[0] = INFINITY;
     ctx->cm_info[1] = ctx->cm_info[2] = tail[0] * ctx->cm_tau * ctx->cm_tau;
     ctx->cm_info[3] = 0.0;
@@ -260,8 +274,9 @@ int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e
   double scaled = 0.0;
   for (int k = 0; k <= kst; ++k) scaled += h[k];
   const double t = std::sqrt(T * std::pow(2.0, -0.5 * kst));
-  launch_cm_apply(ctx->st, p.d_all, nb, p.max_p, (float)t, ctx->stream);
+  launch_cm_apply(ctx->st, p.d_all, nb, p.max_p, (float)t, ctx->d_cm_scale, ctx->stream);
   CK(hipGetLastError());
+  ctx->cm_have_scale = true;
   ctx->cm_info[0] = t;
   ctx->cm_info[1] = h[0] > 0.0 ? INFINITY : tail[0] * ctx->cm_tau * ctx->cm_tau;  // (omega eps)^2 of the mode
   ctx->cm_info[2] = (std::pow(2.0, -0.5 * kst) * scaled + tail[kst]) * ctx->cm_tau * ctx->cm_tau;

@@ -203,7 +203,10 @@ int64_t net_scratch_doubles(int64_t n);
 #define CM_NC 96
 void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, float inv_T, unsigned long long* part,
                     unsigned long long* out, hipStream_t s);
-void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, hipStream_t s);
+void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, float* scale,
+                     hipStream_t s);
+void launch_cm_rescale(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, const float* scale,
+                       hipStream_t s);
 void launch_uniforms(const DevState& st, const int32_t* branches, int32_t nb, uint64_t seed, hipStream_t s);
 // mode 0 exact f32 MFMA, 1 bf16 MFMA, 2 f32-accurate bf16 planes (kernels_wx.hip)
 void launch_fused_grad_wx(const DevState& st, const GradItem* items, int32_t nitems, int32_t act, int mode,

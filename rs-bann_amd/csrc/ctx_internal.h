@@ -140,7 +140,9 @@ struct bann_ctx {
   double* d_netpart = nullptr; // network mode: rss block partials
   int32_t netrss_cap = 0;
   // network mode: the common-mode step-size rule (bann_set_network_step_rule)
-  int32_t cm_rule = 1;
+  int32_t cm_rule = 1;           // 0 off, 1 adapt before every trajectory, 2 frozen (bann_set_network_step_rule)
+  float* d_cm_scale = nullptr;    // the last adapted per-parameter step factors
+  bool cm_have_scale = false;
   float cm_tau = 1.0f;
   float* d_ones = nullptr;                 // n ones: the output error of the common-mode gradient launch
   unsigned long long* d_cm = nullptr;      // per-branch histograms (nbranch x 2 CM_NC), then their sum

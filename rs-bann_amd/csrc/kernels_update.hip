@@ -874,12 +874,27 @@ __global__ void __launch_bounds__(2 * CM_NC) k_cm_sum(const unsigned long long* 
 }
 
 // eps_p *= min(1, t / a_p)
-__global__ void __launch_bounds__(256) k_cm_apply(DevState st, const int32_t* __restrict__ blist, float t) {
+// eps_p *= min(1, t / a_p) (a_p = eps_p |g_p|, left in grad by k_cm_hist); the factor is kept
+// per parameter (scale) for the frozen form of the rule
+__global__ void __launch_bounds__(256) k_cm_apply(DevState st, const int32_t* __restrict__ blist, float t,
+                                                  float* __restrict__ scale) {
   const int b = blist[blockIdx.y];
   const BranchDev bd = st.br[b];
   for (int i = blockIdx.x * 256 + threadIdx.x; i < bd.P; i += gridDim.x * 256) {
     const float a = st.grad[bd.p_off + i];
-    if (a > t) st.eps[bd.p_off + i] *= t / a;
+    const float f = a > t ? t / a : 1.f;
+    if (a > t) st.eps[bd.p_off + i] *= f;
+    scale[bd.p_off + i] = f;
+  }
+}
+// the frozen rule: eps_p *= the factor of the last adapted trajectory (state-independent steps)
+__global__ void __launch_bounds__(256) k_cm_rescale(DevState st, const int32_t* __restrict__ blist,
+                                                    const float* __restrict__ scale) {
+  const int b = blist[blockIdx.y];
+  const BranchDev bd = st.br[b];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < bd.P; i += gridDim.x * 256) {
+    const float f = scale[bd.p_off + i];
+    if (f < 1.f) st.eps[bd.p_off + i] *= f;
   }
 }
 
@@ -890,8 +905,15 @@ void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, flo
   hipLaunchKernelGGL(k_cm_sum, dim3(1), dim3(2 * CM_NC), 0, s, part, nb, out);
 }
 
-void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, hipStream_t s) {
+void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, float* scale,
+                     hipStream_t s) {
   if (nb <= 0) return;
   const unsigned gx = (unsigned)std::min<int64_t>((max_p + 255) / 256, 16);
-  hipLaunchKernelGGL(k_cm_apply, dim3(gx, (unsigned)nb), dim3(256), 0, s, st, branches, t);
+  hipLaunchKernelGGL(k_cm_apply, dim3(gx, (unsigned)nb), dim3(256), 0, s, st, branches, t, scale);
+}
+void launch_cm_rescale(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, const float* scale,
+                       hipStream_t s) {
+  if (nb <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((max_p + 255) / 256, 16);
+  hipLaunchKernelGGL(k_cm_rescale, dim3(gx, (unsigned)nb), dim3(256), 0, s, st, branches, scale);
 }

@@ -350,3 +350,37 @@ def test_common_mode_step_rule(fx_only):
     for b in range(len(specs)):
         assert norm_rel(ctx.get_step_sizes(b), eps_off[b]) < 2e-7
     ctx.close()
+
+
+def test_common_mode_rule_frozen():
+    """bann_set_network_step_rule(2): the step factors adapted before the last trajectory are
+    applied again without recomputing g, so a frozen trajectory's step sizes do not depend on
+    the state it starts from (HMC's reversibility; the sampler adapts during burn-in only):
+    after an adapted trajectory moved the state, the frozen trajectories take bit for bit the
+    adapted step sizes."""
+    rng = np.random.default_rng(13)  # test_common_mode_step_rule's fx-only network: the rule scales
+    n = 1500
+    shapes = [(60, [4, 4, 1], "ridge_ard")] * 8
+    M = sum(m for m, _, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w, prior in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior=prior))))
+        off += m
+    ctx = _context(g, specs, range(len(specs)))
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    y = (sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+         + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    L, c, le = 6, 1.0, 2.0
+    ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=5)
+    info_a = ctx.network_step_rule_info()
+    assert np.isfinite(info_a["threshold"])  # the rule scaled some steps
+    eps_a = [ctx.get_step_sizes(b).copy() for b in range(len(specs))]
+    ctx.set_network_step_rule("frozen")
+    for seed in (6, 7):  # two frozen trajectories from the states the previous ones left
+        ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=seed)
+        for b in range(len(specs)):
+            assert np.array_equal(ctx.get_step_sizes(b), eps_a[b]), b
+    ctx.close()
