@@ -777,6 +777,16 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 // issued once the forward has read it (the head's prediction store first, so
 // the counted wait at the top never waits on a piece younger than the tile).
 // ===========================================================================
+#ifndef FWD_NU
+#define FWD_NU 3  // 8-chunk forward: half-tile units per wave (0: whole-tile slots, the A/B variant)
+#endif
+#ifndef FWD_ABL
+#define FWD_ABL 0  // timing ablations of the ring forward (tools only; results wrong): 1 no MFMA, 2 no head, 4 no stream,
+                  // 8 predictions stored by wave 0 only
+#endif
+#ifndef FWD_PB
+#define FWD_PB 8  // ring forward: tiles per prediction write burst
+#endif
 #ifndef FWD_NS
 #define FWD_NS 2  // tile slots per wave: the stream runs FWD_NS tiles ahead (2: two workgroups per CU;
                   // round 5, network line A/B: 379.6 / 381.2 vs 376.0 / 377.2 steps/s with 4, 376.6 / 378.2 with 3)
@@ -794,14 +804,17 @@ __device__ __forceinline__ void vm_wait_n(int k) {
 #undef VMW
 }
 
-template <int NL, int ACT, int NCH>
-__global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
+// NU > 0 (8-chunk tiles): the half-tile ring, NU units of 4 KiB per wave and the W0 digits in
+// registers (no LDS copy), so that 4 NU KiB per wave set the workgroups per CU
+template <int NL, int ACT, int NCH, int NU>
+__global__ void __launch_bounds__(64 * FX_WAVES, NU > 0 ? 2 : (FWD_NS <= 2 ? 2 : 1))
     k_forward_fx(DevState st, const GradItem* __restrict__ items) {
   constexpr int NH = NL - 1;
   constexpr int NW = FX_WAVES;
   constexpr int NS = FWD_NS;
-  __shared__ __attribute__((aligned(16))) char s_x[NW][NS][FX_SLOT];
-  __shared__ __attribute__((aligned(16))) char s_w0[8 * 1024];
+  static_assert(NU == 0 || NCH == 8, "the half-tile ring needs 8-chunk tiles");
+  __shared__ __attribute__((aligned(16))) char s_x[NW][NU > 0 ? 1 : NS][NU > 0 ? NU * 4096 : FX_SLOT];
+  __shared__ __attribute__((aligned(16))) char s_w0[NU > 0 ? 16 : 8 * 1024];
   __shared__ __attribute__((aligned(16))) float s_hw[NL][20];
 
   const GradItem it = items[blockIdx.x];
@@ -829,14 +842,25 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
   }
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
   float zscale = st.fc[b].scale[g];
-  for (int c = wave; c < nch; c += NW)
-    *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
-        *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+  v4i Areg[NU > 0 ? 8 : 1];  // the ring's W0 digit operands, one per chunk
+  if constexpr (NU > 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) Areg[c] = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+  } else {
+    for (int c = wave; c < nch; c += NW)
+      *reinterpret_cast<v4i*>(&s_w0[c * 1024 + lane * 16]) =
+          *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("" : "+v"(zscale));
   __syncthreads();
   v4i rowsum64 = v4i{0, 0, 0, 0};  // facc[3]'s start (field 3 stored as code - 1)
-  for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
+  if constexpr (NU > 0) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) rowsum64 = fx_rowsum64_acc(Areg[c], rowsum64);
+  } else {
+    for (int c = 0; c < nch; ++c) rowsum64 = fx_rowsum64_acc(*reinterpret_cast<const v4i*>(&s_w0[c * 1024 + lane * 16]), rowsum64);
+  }
   float uWm[NL][4][4], uB[NH][4];  // head weights W_l[j][k] (l >= 1; output layer: k = 0) and biases, scalar
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
@@ -861,9 +885,119 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
   const bool pad_row = 64 * (nch - 1) + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
   auto issue_chunk = [&](int tt, int sl, int c) {
     if (c == nch - 1 && pad_row) return;
-    glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
+    if constexpr (NU == 0) glds16(xsrc + (int64_t)tt * tile_bytes + c * 1024, &s_x[wave][sl][c * 1024]);
   };
 
+  // the head of one tile: in-place fields -> z (one individual per lane) -> f
+  auto head_out = [&](v4i (&facc)[4]) -> float {
+    fx_fwd_fields(facc);
+    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
+    swap32(z0, z2);
+    swap32(z1, z3);
+    swap16(z0, z1);
+    swap16(z2, z3);
+    float a[4];
+    a[0] = act_h_t<ACT>(z0 + uB[0][0]);
+    a[1] = act_h_t<ACT>(z1 + uB[0][1]);
+    a[2] = act_h_t<ACT>(z2 + uB[0][2]);
+    a[3] = act_h_t<ACT>(z3 + uB[0][3]);
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+      float an[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float s = uB[l][k];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s = fmaf(a[j], uWm[l][j][k], s);
+        an[k] = act_h_t<ACT>(s);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = an[k];
+    }
+    float out = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out = fmaf(a[j], uWm[NL - 1][j][0], out);
+    return out;
+  };
+  if constexpr (NU > 0) {
+    // Half-tile ring: NU slots of one 4-chunk unit each (unit u = half u & 1 of the wave's
+    // tile u >> 1); NU - 1 units are in flight while one is read.  A wave owns a contiguous
+    // run of the item's tiles and writes its predictions PB tiles at a time (PB x 256 bytes,
+    // back to back): single 256-byte stores between the stream's reads cost the launch a
+    // fifth of its time (profiles/r05_fwd_store_ablation.md).
+    constexpr int PB = FWD_PB;
+    char* const xw = &s_x[wave][0][0];
+    const int q = (te - tb + NW - 1) / NW;
+    const int tw0 = tb + wave * q;
+    const int nt = te - tw0 < 0 ? 0 : (te - tw0 < q ? te - tw0 : q);
+    const int nu = 2 * nt;
+    auto issue_unit = [&](int u) {
+      if constexpr (FWD_ABL & 4) return;
+      const int64_t tt = tw0 + (u >> 1);
+      char* dst = xw + (u % NU) * 4096;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cc = 4 * (u & 1) + c;
+        if (cc == nch - 1 && pad_row) continue;
+        glds16(xsrc + tt * tile_bytes + cc * 1024, dst + c * 1024);
+      }
+    };
+    for (int u = 0; u < NU && u < nu; ++u) issue_unit(u);
+    for (int k0 = 0; k0 < nt; k0 += PB) {
+      float obuf[PB];
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int k = k0 + j;
+        obuf[j] = 0.f;
+        if (PB > 1 && k >= nt) break;
+        v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int u = 2 * k + h;
+          // younger than unit u: the units issued after it (through u + NU - 1, four pieces
+          // each).  The prediction stores between them are not counted: a store may complete
+          // ahead of older loads, so counting it could release the wait early.
+          const int last = u + NU - 1 < nu - 1 ? u + NU - 1 : nu - 1;
+          if constexpr (!(FWD_ABL & 4)) {
+            if (last == u + NU - 1)
+              asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NU - 1)) : "memory");  // the steady state
+            else
+              vm_wait_n(4 * (last - u));
+          }
+          const char* xs = xw + (u % NU) * 4096;
+          v4u Xq[2];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) Xq[c] = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const v4u Xc = Xq[c % 2];
+            if (c + 2 < 4) Xq[c % 2] = (v4u)lds_tr8_pair(xs + (c + 2) * 1024 + fo0, xs + (c + 2) * 1024 + fo1);
+            if constexpr (FWD_ABL & 1) {
+              facc[c] ^= (v4i)Xc;
+            } else {
+              fx_fwd_chunk(Areg[4 * h + c], Xc, facc);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          // every read of this unit's slot has returned (the MFMAs consumed them): refill it
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (u + NU < nu) issue_unit(u + NU);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FWD_ABL & 2) {
+          obuf[j] = (float)(facc[0].x ^ facc[1].y ^ facc[2].z ^ facc[3].w);
+        } else {
+          obuf[j] = head_out(facc);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int64_t row = 64 * (int64_t)(tw0 + k0 + j) + iota;
+        if (k0 + j < nt && row < n && (!(FWD_ABL & 8) || wave == 0)) predb[row] = obuf[j];
+      }
+    }
+  } else {
   // ring of NS slots: tile i of this wave in slot i % NS; the prologue fills the
   // ring, each iteration refills the slot it consumed with the tile NS ahead
   int tt = tb + wave, sl = 0;
@@ -903,40 +1037,16 @@ __global__ void __launch_bounds__(64 * FX_WAVES, FWD_NS <= 2 ? 2 : 1)
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    fx_fwd_fields(facc);
-    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
-    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
-    swap32(z0, z2);
-    swap32(z1, z3);
-    swap16(z0, z1);
-    swap16(z2, z3);
-    float a[4];
-    a[0] = act_h_t<ACT>(z0 + uB[0][0]);
-    a[1] = act_h_t<ACT>(z1 + uB[0][1]);
-    a[2] = act_h_t<ACT>(z2 + uB[0][2]);
-    a[3] = act_h_t<ACT>(z3 + uB[0][3]);
-#pragma unroll
-    for (int l = 1; l < NH; ++l) {
-      float an[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float s = uB[l][k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s = fmaf(a[j], uWm[l][j][k], s);
-        an[k] = act_h_t<ACT>(s);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = an[k];
+    {
+      const float out = head_out(facc);
+      const int64_t row = 64 * (int64_t)tt + iota;
+      if (row < n) predb[row] = out;
     }
-    float out = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) out = fmaf(a[j], uWm[NL - 1][j][0], out);
-    const int64_t row = 64 * (int64_t)tt + iota;
-    if (row < n) predb[row] = out;
     // every read of this slot has returned (the MFMAs consumed them): refill it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (tt + NS * NW < te)
       for (int c = 0; c < nch; ++c) issue_chunk(tt + NS * NW, sl, c);
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -945,11 +1055,11 @@ template <int NL, int NCH>
 static void launch_fwd_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, hipStream_t s) {
   const dim3 grid((unsigned)nitems), block(64 * FX_WAVES);
   switch (act) {
-    case 0: hipLaunchKernelGGL((k_forward_fx<NL, 0, NCH>), grid, block, 0, s, st, items); break;
-    case 1: hipLaunchKernelGGL((k_forward_fx<NL, 1, NCH>), grid, block, 0, s, st, items); break;
-    case 2: hipLaunchKernelGGL((k_forward_fx<NL, 2, NCH>), grid, block, 0, s, st, items); break;
-    case 3: hipLaunchKernelGGL((k_forward_fx<NL, 3, NCH>), grid, block, 0, s, st, items); break;
-    default: hipLaunchKernelGGL((k_forward_fx<NL, 4, NCH>), grid, block, 0, s, st, items); break;
+    case 0: hipLaunchKernelGGL((k_forward_fx<NL, 0, NCH, NCH == 8 ? FWD_NU : 0>), grid, block, 0, s, st, items); break;
+    case 1: hipLaunchKernelGGL((k_forward_fx<NL, 1, NCH, NCH == 8 ? FWD_NU : 0>), grid, block, 0, s, st, items); break;
+    case 2: hipLaunchKernelGGL((k_forward_fx<NL, 2, NCH, NCH == 8 ? FWD_NU : 0>), grid, block, 0, s, st, items); break;
+    case 3: hipLaunchKernelGGL((k_forward_fx<NL, 3, NCH, NCH == 8 ? FWD_NU : 0>), grid, block, 0, s, st, items); break;
+    default: hipLaunchKernelGGL((k_forward_fx<NL, 4, NCH, NCH == 8 ? FWD_NU : 0>), grid, block, 0, s, st, items); break;
   }
 }
 
