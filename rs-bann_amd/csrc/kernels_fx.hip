@@ -785,7 +785,8 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
                   // 8 predictions stored by wave 0 only
 #endif
 #ifndef FWD_PB
-#define FWD_PB 8  // ring forward: tiles per prediction write burst
+#define FWD_PB 8  // ring forward: tiles per prediction write burst (1: one store per tile, counted in the waits:
+                  // kbench 1.134 vs 1.173 ms, but 1.203 vs 1.181 ms inside the network trajectory)
 #endif
 #ifndef FWD_NS
 #define FWD_NS 2  // tile slots per wave: the stream runs FWD_NS tiles ahead (2: two workgroups per CU;
@@ -956,15 +957,21 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NU > 0 ? 2 : (FWD_NS <= 2 ? 2 :
         for (int h = 0; h < 2; ++h) {
           const int u = 2 * k + h;
           // younger than unit u: the units issued after it (through u + NU - 1, four pieces
-          // each).  The prediction stores between them are not counted: a store may complete
-          // ahead of older loads, so counting it could release the wait early.
+          // each) and, with one prediction store per tile (PB = 1), the stores of tiles kb
+          // that ended after u was issued (tile kb stores right after issuing unit
+          // 2 kb + 1 + NU): kb in [ceil((u - NU - 1) / 2), floor((u - 2) / 2)].  Vector memory
+          // operations leave vmcnt in issue order on gfx9 (loads, stores and LDS-DMA alike),
+          // so counting them is exact; a wait that left the stores out would also wait for
+          // them, i.e. for the whole ring behind a store to HBM (profiles/r05_fwd_store_ablation.md).
+          // The stores of tiles before a wave's last are full (every row < n), so each is one
+          // issued instruction.
           const int last = u + NU - 1 < nu - 1 ? u + NU - 1 : nu - 1;
-          if constexpr (!(FWD_ABL & 4)) {
-            if (last == u + NU - 1)
-              asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NU - 1)) : "memory");  // the steady state
-            else
-              vm_wait_n(4 * (last - u));
+          int younger_st = 0;
+          if constexpr (PB == 1 && !(FWD_ABL & 8)) {
+            const int lo = u - NU - 1 <= 0 ? 0 : (u - NU) >> 1, hi = (u - 2) >> 1;
+            younger_st = u >= 2 && hi >= lo ? hi - lo + 1 : 0;
           }
+          if constexpr (!(FWD_ABL & 4)) vm_wait_n(4 * (last - u) + younger_st);
           const char* xs = xw + (u % NU) * 4096;
           v4u Xq[2];
 #pragma unroll
