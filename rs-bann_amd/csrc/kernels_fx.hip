@@ -788,6 +788,9 @@ void launch_fused_grad_fx(const DevState& st, const GradItem* items, int32_t nit
 #define FWD_PB 8  // ring forward: tiles per prediction write burst (1: one store per tile, counted in the waits:
                   // kbench 1.134 vs 1.173 ms, but 1.203 vs 1.181 ms inside the network trajectory)
 #endif
+#ifndef FWD_PBC
+#define FWD_PBC 0  // PB > 1: count the bursts' stores in the waits too
+#endif
 #ifndef FWD_NS
 #define FWD_NS 2  // tile slots per wave: the stream runs FWD_NS tiles ahead (2: two workgroups per CU;
                   // round 5, network line A/B: 379.6 / 381.2 vs 376.0 / 377.2 steps/s with 4, 376.6 / 378.2 with 3)
@@ -967,9 +970,10 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NU > 0 ? 2 : (FWD_NS <= 2 ? 2 :
           // issued instruction.
           const int last = u + NU - 1 < nu - 1 ? u + NU - 1 : nu - 1;
           int younger_st = 0;
-          if constexpr (PB == 1 && !(FWD_ABL & 8)) {
+          if constexpr ((PB == 1 || FWD_PBC) && !(FWD_ABL & 8)) {
             const int lo = u - NU - 1 <= 0 ? 0 : (u - NU) >> 1, hi = (u - 2) >> 1;
-            younger_st = u >= 2 && hi >= lo ? hi - lo + 1 : 0;
+            if (u >= 2)  // PB > 1: the tiles that end a burst (kb % PB == PB - 1) store PB rows of 64
+              for (int kb = lo; kb <= hi; ++kb) younger_st += (PB == 1 || kb % PB == PB - 1) ? PB : 0;
           }
           if constexpr (!(FWD_ABL & 4)) vm_wait_n(4 * (last - u) + younger_st);
           const char* xs = xw + (u % NU) * 4096;
