@@ -159,6 +159,11 @@ def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net
         library_comm()
     info = ctx.comm_info()
     factor = 0.5 * default_step_factor(args.config, "network", args.hidden_bf16, L, args.network_step_rule)
+    # warm: one untimed trajectory first (it adapts the common-mode rule's factors, the
+    # library's auto mode; kernels and the communicator's first collective are loaded),
+    # then the timed one, which applies the factors frozen
+    ctx.network_hmc_step(y_net, L, bias=0.0, lambda_e=2.0, step_mode="izmailov", step_factor=factor, seed=29)
+    ctx.synchronize()
     ctx.set_launch_timing(True)
     if dist is not None:
         dist.barrier()
@@ -181,7 +186,9 @@ def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net
         ranks_seen = [float(tr[0])]
     el, ar_ms, fwd_ms, grad_ms, upd_ms = vals
     rule = ctx.network_step_rule_info()
+    rule_state = ctx.network_step_rule_state()
     return {"step_rule": {"kind": args.network_step_rule, "tau": args.network_tau,
+                          "timed_trajectory": "frozen" if rule_state["frozen"] else rule_state["mode"],
                           "fraction_scaled": rule["fraction_scaled"], "mode_before": _fin(rule["mode_before"]),
                           "mode_after": _fin(rule["mode_after"])},
             "n_gpus": world, "comm": info["kind"] if info["kind"] == "rccl" else f"callback ({backend})",
@@ -190,7 +197,7 @@ def network_check(ctx, dist, dist_dev, world, rank, backend, library_comm, y_net
             "steps_per_s": L / el, "allreduces": n_ar, "allreduce_us_per_step": 1e3 * ar_ms,
             "allreduce_bytes": 4 * len(y_net), "forward_ms": fwd_ms, "gradient_ms": grad_ms, "update_ms": upd_ms,
             "dH": r["trace"][-1] - r["trace"][0], "branches_per_rank": nb,
-            "timing": "HIP events on the library stream, max over ranks"}
+            "timing": "HIP events on the library stream, max over ranks; warm (after one untimed trajectory)"}
 
 
 def launch_ranks(nproc: int) -> int:
@@ -327,7 +334,10 @@ def main():
     for k in range(nb):
         ctx.add_branch(np.arange(k * m_b, (k + 1) * m_b, dtype=np.int32), widths, "tanh", "ridge_ard")
     ctx.finalize(free_raw=True)
-    ctx.set_network_step_rule(args.network_step_rule != "off", args.network_tau)
+    # the library default (auto): the first trajectory adapts the common-mode factors, every later
+    # one applies them frozen (state-independent step sizes); "adaptive" re-adapts before every one
+    ctx.set_network_step_rule({"common_mode": "auto", "adaptive": "adaptive", "off": "off"}[args.network_step_rule],
+                              args.network_tau)
     path = ctx.kernel_path(0)
     assert path == ("layered" if heavy else "wide" if widths[0] > 4 else "fused" if m_b <= 512 else "fused_large")
     assert all(ctx.kernel_path(k) == path for k in range(nb))
@@ -376,6 +386,20 @@ def main():
     del preds
     ctx.synchronize()
     setup_s = time.time() - t_setup
+
+    # every rank's branch count must be its shard_ranges entry, every rank present once
+    # (a mis-ranked launch -- duplicate RANKs, a wrong WORLD_SIZE -- exits non-zero)
+    if dist is not None:
+        import torch
+        sh = torch.zeros(2 * world, device=dist_dev, dtype=torch.float64)
+        sh[rank], sh[world + rank] = float(nb), 1.0
+        dist.all_reduce(sh)
+        want = [float(e - s_) for s_, e in shard_ranges([m_b] * B_total, max(world, args.emulate_shard))[:world]]
+        got, seen_r = [float(v) for v in sh[:world]], [float(v) for v in sh[world:]]
+        if seen_r != [1.0] * world or got != want:
+            log(f"rank {rank}: shard check failed: branches per rank {got}, shard_ranges {want}, ranks seen {seen_r}")
+            sys.stdout.flush()
+            os._exit(5)
 
     def library_comm():
         """the library's communicator: RCCL over xGMI (one GPU per rank), or a gloo
@@ -457,6 +481,13 @@ def main():
         wd.cancel()
         if rank == 0:
             log(json.dumps({"network_check": netcheck}))
+        # a mis-ranked run must not publish a line: RCCL's own rank count (MIN over ranks)
+        # has to be the launch's world size
+        if netcheck["comm_ranks_reported"] != world:
+            log(f"network_check: the communicator reports {netcheck['comm_ranks_reported']} ranks, "
+                f"the launch has {world}")
+            sys.stdout.flush()
+            os._exit(5)
         # the library leaves every branch's target at its Gibbs target of the state the
         # check ended in (accepted: its last step; otherwise theta_0) and the device
         # residual at y - sum_b f_b (include/bann.h): the branch line samples from there
@@ -487,11 +518,9 @@ def main():
         b2b_grad_ms, b2b_upd_ms = b2b_session(restore=True)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
-    if args.sampler == "network" and args.network_step_rule == "common_mode":
-        # the rule adapted its step factors during the warmup (burn-in); the timed and the
-        # acceptance trajectories sample with them frozen: step sizes independent of each
-        # trajectory's start, as HMC's reversibility asks (bann_set_network_step_rule)
-        ctx.set_network_step_rule("frozen", args.network_tau)
+    # network sampler, common-mode rule (auto): the warmup trajectory adapted the step factors
+    # (burn-in); the timed and the acceptance trajectories apply them frozen -- step sizes
+    # independent of each trajectory's start, as HMC's reversibility asks
     if args.sampler == "branch":
         b2b_grad_ms, b2b_upd_ms = b2b_session(restore=False)
     timing = args.sampler in ("branch", "network") and not args.no_launch_timing

@@ -60,8 +60,20 @@ typedef enum {
 /* HMCStepResult (branch_sampler.rs:1310-1314) */
 typedef enum { BANN_ACCEPTED = 0, BANN_REJECTED = 1, BANN_REJECTED_EARLY = 2 } bann_hmc_status;
 
-/* StepSizeMode (mcmc_cfg.rs:264-270); INJECTED = caller supplies eps */
-typedef enum { BANN_STEP_UNIFORM = 0, BANN_STEP_RANDOM = 1, BANN_STEP_IZMAILOV = 3, BANN_STEP_INJECTED = 100 } bann_step_mode;
+/* StepSizeMode (mcmc_cfg.rs:264-270); INJECTED = caller supplies eps.
+ * STD_SCALED (branch_sampler.rs:1213): eps = c * sqrt(1 / lambda_l) per weight layer and
+ * c * (1 / sqrt(lambda_b)) per bias layer in f32 (ridge_base.rs:52-82, lasso_base.rs:53-82,
+ * std_normal_branch.rs:51-80).  The ARD priors return EMPTY step-size vectors there
+ * (ridge_ard.rs:56-68, lasso_ard.rs:62-74: hmc_step would index-panic), so it is refused
+ * (BANN_E_ARG) for a branch with an ARD prior.  Joint HMC falls back to random step sizes
+ * as the reference does (branch_sampler.rs:1092-1101). */
+typedef enum {
+  BANN_STEP_UNIFORM = 0,
+  BANN_STEP_RANDOM = 1,
+  BANN_STEP_STD_SCALED = 2,
+  BANN_STEP_IZMAILOV = 3,
+  BANN_STEP_INJECTED = 100
+} bann_step_mode;
 
 /* ---------------- context ---------------- */
 int bann_ctx_create(int device, bann_ctx** out);
@@ -394,7 +406,8 @@ int bann_exchange_residual_device(bann_ctx* ctx);
  *   shared with every rank through the -H all-reduce, so all ranks decide alike.
  * Per step the first pass over the genotypes is forward-only (the outputs the
  * all-reduce needs); the gradient pass follows once e is known.
- * Outputs (may be NULL): status, h_trace[L+1], rss of the final state.  On
+ * Outputs (may be NULL): status, h_trace[L+1], rss of the final state (theta_L
+ * if accepted, theta_0 otherwise).  On
  * return (accepted: theta_L, otherwise theta_0) every local branch's target is
  * its Gibbs target y_b = f_b - e = y - bias - sum_{c != b} f_c over all ranks
  * (net.rs:279-280), and the context's device residual is y - bias - sum_b f_b. */
@@ -406,18 +419,29 @@ int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, float lambd
  * sampler is this library's).  With per-branch Izmailov / uniform
  * steps the joint leapfrog's stiffest direction is the common mode -- every branch
  * shifting the network output together -- whose curvature grows with the number
- * of branches B (B aligned branches: B times one branch's).  common_mode = 1
- * (default, tau = 1): before each trajectory one extra gradient launch with output
- * error 1 gives g = J^T 1 (the gradient of sum_i F_i) and every step size becomes
- * eps_p min(1, t / (eps_p |g_p|)) with the largest t (within 2^(1/4)) such that
- * lambda_e / n sum_p min(eps_p |g_p|, t)^2 <= tau^2: the common mode runs at
- * omega eps <= tau while the parameters that do not drive it keep their steps.
- * Summed over the ranks (collective); not applied to injected step sizes.
- * common_mode = 2 (frozen): the factors of the last adapted trajectory are applied
- * again without recomputing g -- step sizes that do not depend on the trajectory's
- * start, as HMC's reversibility asks; the sampler adapts during burn-in (1) and
- * samples frozen (2), as bench.py does.  0 = off. */
+ * of branches B (B aligned branches: B times one branch's).  Adapting: one extra
+ * gradient launch with output error 1 gives g = J^T 1 (the gradient of sum_i F_i)
+ * and every step size becomes eps_p min(1, t / (eps_p |g_p|)) with the largest t
+ * (within 2^(1/4)) such that lambda_e / n sum_p min(eps_p |g_p|, t)^2 <= tau^2: the
+ * common mode runs at omega eps <= tau while the parameters that do not drive it
+ * keep their steps.  Summed over the ranks (collective); not applied to injected
+ * step sizes.  Frozen: the per-parameter factors of the last adapted trajectory are
+ * applied again without recomputing g -- step sizes that do not depend on the
+ * trajectory's start, as HMC's reversibility asks.
+ *   common_mode = 3 (DEFAULT, tau = 1): auto -- the first K trajectories adapt
+ *     (K = 1 unless bann_set_network_adapt_trajectories says otherwise; burn-in),
+ *     every later one is frozen.  Setting mode 3 again restarts the adaptation.
+ *   common_mode = 2: frozen (adapts once if nothing was adapted yet).
+ *   common_mode = 1: adapt before EVERY trajectory -- the proposal then depends on
+ *     theta_0 and detailed balance does not hold: a diagnostic, not a sampler.
+ *   common_mode = 0: off (plain per-branch steps). */
 int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau);
+/* auto mode (3): the number K >= 1 of adapting trajectories before the factors freeze;
+ * restarts the adaptation */
+int bann_set_network_adapt_trajectories(bann_ctx* ctx, int32_t k);
+/* the rule's state: mode, adapting trajectories done in auto mode, and whether the NEXT
+ * trajectory applies frozen factors (1) or adapts / runs without the rule (0) */
+int bann_network_step_rule_state(const bann_ctx* ctx, int32_t* mode, int32_t* adapted, int32_t* frozen);
 /* the last network trajectory's rule: [threshold t (inf: no step changed),
  * (omega eps)^2 of the common mode before (inf when some single parameter alone
  * exceeded tau) and after, the fraction of parameters whose step was reduced] */

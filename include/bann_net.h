@@ -53,8 +53,10 @@ typedef struct {
   float hmc_step_size_factor;
   float hmc_max_hamiltonian_error;
   int32_t hmc_integration_length;
-  int32_t hmc_step_size_mode; /* bann_step_mode: BANN_STEP_IZMAILOV, BANN_STEP_UNIFORM or BANN_STEP_RANDOM
-                                 (StepSizeMode, mcmc_cfg.rs:264-270; StdScaled is unusable in the reference) */
+  int32_t hmc_step_size_mode; /* bann_step_mode: BANN_STEP_IZMAILOV, BANN_STEP_UNIFORM, BANN_STEP_RANDOM or
+                                 BANN_STEP_STD_SCALED (StepSizeMode, mcmc_cfg.rs:264-270); StdScaled is
+                                 refused for ARD-prior branches, whose reference step sizes are empty
+                                 (ridge_ard.rs:56-68, lasso_ard.rs:62-74); joint HMC uses random sizes */
   int32_t chain_length;
   int32_t burn_in;
   int32_t fixed_param_precisions;

@@ -497,6 +497,32 @@ def izmailov_step_sizes(br: Branch, c: float, L_int: int):
     return eps_w, eps_b
 
 
+def std_scaled_step_sizes(br: Branch, c: float):
+    """StdScaled step sizes (StepSizeMode::StdScaled, dispatched at branch_sampler.rs:1213).
+
+    ridge_base.rs:52-82, lasso_base.rs:53-82, std_normal_branch.rs:51-80, in f32 as the
+    reference computes them: weights c * (1 / lambda_l).sqrt() (a host f32 scalar),
+    biases c * (1 / sqrt(lambda_b)) (ArrayFire f32; lasso_base's 1 * c * (1 / sqrt) is the
+    same value).  The ARD priors return EMPTY vectors (ridge_ard.rs:56-68,
+    lasso_ard.rs:62-74), on which the reference's leapfrog index-panics: ValueError here.
+    Returns (eps_w, eps_b) as full-shape float32 arrays."""
+    if br.prior in ARD_PRIORS:
+        raise ValueError("StdScaled step sizes are empty for the ARD priors (ridge_ard.rs:56-68)")
+    f32 = np.float32
+    cc = f32(c)
+    eps_w = []
+    for l in range(br.num_layers):
+        lam = f32(np.asarray(br.weight_precisions[l], dtype=np.float32).reshape(-1)[0])
+        e = f32(cc * np.sqrt(f32(f32(1.0) / lam), dtype=np.float32))
+        eps_w.append(np.full(br.weights[l].shape, e, dtype=np.float32))
+    eps_b = []
+    for l in range(br.num_layers - 1):
+        lamb = f32(np.asarray(br.bias_precisions[l], dtype=np.float32).reshape(-1)[0])
+        e = f32(cc * f32(f32(1.0) / np.sqrt(lamb, dtype=np.float32)))
+        eps_b.append(np.full(br.biases[l].shape, e, dtype=np.float32))
+    return eps_w, eps_b
+
+
 def uniform_step_sizes(br: Branch, c: float):
     """branch_sampler.rs:706-732"""
     return [c * np.ones(w.shape) for w in br.weights], [c * np.ones(b.shape) for b in br.biases]

@@ -177,6 +177,10 @@ class NetOracle:
                         ew, eb = O.izmailov_step_sizes(br, factor, L_int)
                     elif step_mode == "uniform":
                         ew, eb = O.uniform_step_sizes(br, factor)
+                    elif step_mode == "std_scaled":   # branch_sampler.rs:1213, ridge_base.rs:52-82
+                        ew, eb = O.std_scaled_step_sizes(br, factor)
+                        ew = [np.asarray(e, np.float64) for e in ew]
+                        eb = [np.asarray(e, np.float64) for e in eb]
                     out = O.hmc_step(br, self.X[b], target, ew, eb, p_w, p_b, L_int, max_dH, u)
                 self.ns += 1
                 self.nacc += out["status"] == O.ACCEPTED

@@ -20,7 +20,7 @@ STATUS = {0: "BANN_OK", -1: "BANN_E_HIP", -2: "BANN_E_SHAPE", -3: "BANN_E_OOM", 
           -5: "BANN_E_ARG"}
 ACTIVATIONS = {"tanh": 0, "relu": 1, "leaky_relu": 2, "silu": 3, "identity": 4}
 PRIORS = {"ridge_ard": 0, "ridge_base": 1, "lasso_ard": 2, "lasso_base": 3, "std_normal": 4}
-STEP_MODES = {"uniform": 0, "random": 1, "izmailov": 3, "injected": 100}
+STEP_MODES = {"uniform": 0, "random": 1, "std_scaled": 2, "izmailov": 3, "injected": 100}
 HMC_STATUS = {0: "accepted", 1: "rejected", 2: "rejected_early"}
 
 
@@ -134,6 +134,8 @@ SIGNATURES = {
     "bann_exchange_residual_device": (C.c_int, [_P]),
     "bann_set_network_step_rule": (C.c_int, [_P, _i32, _f32]),
     "bann_network_step_rule_info": (C.c_int, [_P, _pf64]),
+    "bann_set_network_adapt_trajectories": (C.c_int, [_P, _i32]),
+    "bann_network_step_rule_state": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "bann_residual_set": (C.c_int, [_P, _pf32]),
     "bann_residual_get": (C.c_int, [_P, _pf32]),
     "bann_residual_device": (C.c_int, [_P, C.POINTER(_pf32)]),

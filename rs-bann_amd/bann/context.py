@@ -436,13 +436,28 @@ class BannContext:
             C.byref(rss)))
         return dict(status=st.value, trace=tr, rss=rss.value)
 
-    def set_network_step_rule(self, common_mode=True, tau: float = 1.0):
+    def set_network_step_rule(self, common_mode="auto", tau: float = 1.0):
         """the network-joint state's step sizes (bann_set_network_step_rule): the common-mode
-        water-filling rule at omega eps <= tau adapted before every trajectory (True / 1,
-        the default), frozen at the last adapted factors ("frozen" / 2: state-independent
-        steps for sampling after burn-in), or the per-branch steps as given (False / 0)."""
-        mode = 2 if common_mode == "frozen" else int(common_mode)
+        water-filling rule at omega eps <= tau.  "auto" / 3 (the library default): adapted on
+        the first K trajectories (set_network_adapt_trajectories, K = 1), then frozen; "frozen"
+        / 2: the last adapted factors (state-independent steps); "adaptive" / True / 1:
+        re-adapted before every trajectory (state-dependent proposals: a diagnostic);
+        "off" / False / 0: the per-branch steps as given."""
+        names = {"auto": 3, "frozen": 2, "adaptive": 1, "off": 0, True: 1, False: 0}
+        mode = names[common_mode] if isinstance(common_mode, (str, bool)) else int(common_mode)
         self._check(self._lib.bann_set_network_step_rule(self._h, mode, float(tau)))
+
+    def set_network_adapt_trajectories(self, k: int):
+        """auto mode: the number of adapting trajectories before the factors freeze (restarts)."""
+        self._check(self._lib.bann_set_network_adapt_trajectories(self._h, int(k)))
+
+    def network_step_rule_state(self) -> dict:
+        """mode, adapting trajectories done (auto mode), and whether the next trajectory
+        applies frozen factors."""
+        m, a, f = C.c_int32(), C.c_int32(), C.c_int32()
+        self._check(self._lib.bann_network_step_rule_state(self._h, C.byref(m), C.byref(a), C.byref(f)))
+        return dict(mode={0: "off", 1: "adaptive", 2: "frozen", 3: "auto"}[m.value], adapted=a.value,
+                    frozen=bool(f.value))
 
     def network_step_rule_info(self) -> dict:
         """the last network trajectory's rule: threshold t, (omega eps)^2 of the common mode

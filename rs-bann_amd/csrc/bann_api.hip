@@ -128,6 +128,29 @@ static void host_random_step_sizes(const BranchHost& h, float c, std::mt19937_64
   for (auto& e : eps) e = U(rng) * f;
 }
 
+// StdScaled step sizes (dispatched at branch_sampler.rs:1213) for the Base priors:
+// ridge_base.rs:52-82, lasso_base.rs:53-82, std_normal_branch.rs:51-80 -- in f32 as the
+// reference: weights c * (1 / lambda_l).sqrt() (host scalar), biases
+// c * (1 / sqrt(lambda_b)) (the lasso form 1 * c * (1 / sqrt) rounds identically).
+// The ARD priors return empty vectors (ridge_ard.rs:56-68, lasso_ard.rs:62-74): refused.
+static bool host_std_scaled_step_sizes(const BranchHost& h, float c, std::vector<float>& eps) {
+  if (h.prior == BANN_RIDGE_ARD || h.prior == BANN_LASSO_ARD) return false;
+  const BranchDev& d = h.dev;
+  eps.assign(h.P, 0.f);
+  for (int l = 0; l < h.L; ++l) {
+    const volatile float inv = 1.f / h.prec[l];
+    const float e = c * sqrtf(inv);
+    const int cnt = d.win[l] * d.widths[l];
+    for (int k = 0; k < cnt; ++k) eps[d.woff[l] + k] = e;
+  }
+  for (int l = 0; l < h.L - 1; ++l) {
+    const volatile float rs = 1.f / sqrtf(h.prec[h.L + l]);
+    const float e = c * rs;
+    for (int k = 0; k < d.widths[l]; ++k) eps[d.boff[l] + k] = e;
+  }
+  return true;
+}
+
 // per-parameter Izmailov step base, so the device can form eps = base * c / L
 // for any factor c and trajectory length L without a host round trip:
 // ridge / bias terms pi / (2 sqrt(lam)), lasso 1 / (4 lam); negative = the
@@ -218,6 +241,7 @@ int build_plan(bann_ctx* ctx, const int32_t* branches, int32_t nb, Plan& p, bool
       key.L = h.L;
       key.cpw = fxl_cpw(d.nchunks);
       key.nw = (d.nchunks + key.cpw - 1) / key.cpw;
+      key.head = ctx->fxl_head ? 1 : 0;
       key.full = d.nchunks == key.cpw * key.nw;
     } else if (d.fused == 2) {  // wx: (act, marker chunks: the plane kernel is compiled per chunk count)
       key.nw = d.nchunks;
@@ -389,7 +413,7 @@ int run_grad(bann_ctx* ctx, const Plan& p, int write_pred, int upd_mode, int upd
     if (g.kind == 2)
       launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, wp, ctx->stream);
     else if (g.kind == 3)
-      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, wp, ctx->stream);
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, wp, g.head, ctx->stream);
     else
       launch_fused_grad_fx(s, g.d_items, ni, g.L, g.act, g.full, wp, upd_mode, upd_step, cnt, fo, ctx->stream);
   }
@@ -420,7 +444,7 @@ int run_forward(bann_ctx* ctx, const Plan& p) {
     if (g.kind == 2)
       launch_fused_grad_wx(s, g.d_items, ni, g.act, ctx->wide_bf16 ? 1 : (wx_exact() ? 0 : 2), g.nw, 1, ctx->stream);
     else if (g.kind == 3)
-      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, 1, ctx->stream);
+      launch_fused_grad_fxl(s, g.d_items, ni, g.L, g.act, g.nw, g.cpw, g.full, 1, g.head, ctx->stream);
     else if (g.fi)
       launch_forward_fi(s, g.d_items, ni, g.tiles, g.L, g.act, g.max_seg, ctx->cus, ctx->stream);
     else
@@ -479,6 +503,7 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   bann_ctx* ctx = new bann_ctx();
   ctx->device = device;
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
+  if (const char* e = getenv("BANN_FXL_HEAD")) ctx->fxl_head = atoi(e) != 0;
   if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -1130,6 +1155,8 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   ctx->pred_ok.assign(ctx->br.size(), 0);
   int rc = ensure_htrace(ctx, 1);
   if (rc) return rc;
+  rc = net_buffers_init(ctx);  // the network sampler allocates nothing inside its trajectories
+  if (rc) return rc;
   refresh_state(ctx);
   CK(hipStreamSynchronize(ctx->stream));
   if (free_raw) {
@@ -1566,9 +1593,16 @@ int traj_prepare(bann_ctx* ctx, const Plan& p, int32_t L, float max_dh, int32_t 
       if (!eps) return fail(ctx, BANN_E_ARG, "injected step sizes need eps");
       CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, eps + off, h.P * sizeof(float), hipMemcpyHostToDevice,
                         ctx->stream));
+    } else if (step_mode == BANN_STEP_STD_SCALED) {
+      if (!host_std_scaled_step_sizes(h, factor, e))
+        return fail(ctx, BANN_E_ARG,
+                    "StdScaled step sizes are empty for the ARD priors in the reference (ridge_ard.rs:56-68, "
+                    "lasso_ard.rs:62-74; hmc_step would index-panic): use Izmailov, uniform or random");
+      CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, e.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
+                        ctx->stream));
+      CK(hipStreamSynchronize(ctx->stream));  // e is reused for the next branch
     } else {
-      if (step_mode != BANN_STEP_RANDOM)
-        return fail(ctx, BANN_E_ARG, "unsupported step size mode (StdScaled is not usable in the reference either)");
+      if (step_mode != BANN_STEP_RANDOM) return fail(ctx, BANN_E_ARG, "unknown step size mode");
       host_random_step_sizes(h, factor, rng, e);
       CK(hipMemcpyAsync(ctx->d_eps + h.dev.p_off, e.data(), h.P * sizeof(float), hipMemcpyHostToDevice,
                         ctx->stream));
@@ -1648,7 +1682,7 @@ static std::string traj_graph_key(const bann_ctx* ctx, const Plan& p, int32_t L)
   put((int64_t)(intptr_t)p.d_gx);
   put((int64_t)(intptr_t)p.d_gxpre);
   for (const auto& g : p.groups) {
-    put(g.kind), put(g.L), put(g.act), put(g.nw), put(g.cpw), put(g.full);  // cpw: fxl's template and LDS size
+    put(g.kind), put(g.L), put(g.act), put(g.nw), put(g.cpw), put(g.full), put(g.head);  // cpw, head: fxl's kernel
     put((int64_t)g.items.size());
     put((int64_t)(intptr_t)g.d_items);
   }

@@ -187,11 +187,62 @@ extern "C" int bann_exchange_residual_device(bann_ctx* ctx) {
 
 extern "C" int bann_set_network_step_rule(bann_ctx* ctx, int32_t common_mode, float tau) {
   if (!ctx) return BANN_E_ARG;
-  if (common_mode < 0 || common_mode > 2) return fail(ctx, BANN_E_ARG, "common_mode: 0 off, 1 adapt, 2 frozen");
+  if (common_mode < 0 || common_mode > 3)
+    return fail(ctx, BANN_E_ARG, "common_mode: 0 off, 1 adapt every trajectory, 2 frozen, 3 auto");
   if (common_mode && !(tau > 0.f)) return fail(ctx, BANN_E_ARG, "tau must be positive");
-  if (common_mode == 1 && ctx->cm_tau != tau) ctx->cm_have_scale = false;
+  if ((common_mode == 1 || common_mode == 3) && ctx->cm_tau != tau) ctx->cm_have_scale = false;
+  if (common_mode == 3) ctx->cm_adapted = 0;  // auto: adapt afresh, then freeze
   ctx->cm_rule = common_mode;
   ctx->cm_tau = tau;
+  return BANN_OK;
+}
+
+extern "C" int bann_set_network_adapt_trajectories(bann_ctx* ctx, int32_t k) {
+  if (!ctx) return BANN_E_ARG;
+  if (k < 1) return fail(ctx, BANN_E_ARG, "at least one adapting trajectory");
+  ctx->cm_adapt_total = k;
+  ctx->cm_adapted = 0;
+  return BANN_OK;
+}
+
+extern "C" int bann_network_step_rule_state(const bann_ctx* ctx, int32_t* mode, int32_t* adapted, int32_t* frozen) {
+  if (!ctx) return BANN_E_ARG;
+  if (mode) *mode = ctx->cm_rule;
+  if (adapted) *adapted = ctx->cm_adapted;
+  // the next trajectory takes the stored factors without recomputing them
+  const bool fz = ctx->cm_have_scale &&
+                  (ctx->cm_rule == 2 || (ctx->cm_rule == 3 && ctx->cm_adapted >= ctx->cm_adapt_total));
+  if (frozen) *frozen = fz ? 1 : 0;
+  return BANN_OK;
+}
+
+// the network sampler's buffers (bann_finalize): the error / sum n-vectors, the rss
+// trace, the common-mode rule's factors, ones and histograms.  Nothing is allocated
+// or uploaded synchronously inside bann_network_hmc_step (but a longer L grows the
+// rss trace once).
+int net_buffers_init(bann_ctx* ctx) {
+  const int64_t n = ctx->n;
+  if (!ctx->d_netsum) {
+    CK(dalloc(&ctx->d_netsum, n));
+    CK(dalloc(&ctx->d_nety, n));
+    CK(dalloc(&ctx->d_netpart, net_scratch_doubles(n)));
+  }
+  if (ctx->netrss_cap < 129) {
+    dfree(ctx->d_netrss);
+    ctx->d_netrss = nullptr;
+    CK(dalloc(&ctx->d_netrss, 129));
+    ctx->netrss_cap = 129;
+  }
+  if (!ctx->d_cm_scale && !ctx->br.empty()) {
+    const BranchHost& last = ctx->br.back();
+    CK(dalloc(&ctx->d_cm_scale, last.dev.p_off + last.P));
+  }
+  if (!ctx->d_ones) {
+    CK(dalloc(&ctx->d_ones, n));
+    launch_fill_f32(ctx->d_ones, 1.f, n, ctx->stream);
+    CK(hipGetLastError());
+    CK(dalloc(&ctx->d_cm, ((int64_t)ctx->br.size() + 1) * 2 * CM_NC));
+  }
   return BANN_OK;
 }
 
@@ -209,28 +260,25 @@ namespace {
 int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e) {
   const int64_t n = ctx->n;
   const int32_t nb = (int32_t)p.all.size();
-  if (!ctx->d_cm_scale) {
-    const BranchHost& last = ctx->br.back();
-    CK(dalloc(&ctx->d_cm_scale, last.dev.p_off + last.P));
-  }
-  if (ctx->cm_rule == 2 && ctx->cm_have_scale) {  // frozen: the adapted factors, no gradient launch
+  int rc = net_buffers_init(ctx);  // no-op after bann_finalize
+  if (rc) return rc;
+  const bool frozen = ctx->cm_have_scale &&
+                      (ctx->cm_rule == 2 || (ctx->cm_rule == 3 && ctx->cm_adapted >= ctx->cm_adapt_total));
+  if (frozen) {  // the adapted factors, no gradient launch: step sizes independent of theta_0
     launch_cm_rescale(ctx->st, p.d_all, nb, p.max_p, ctx->d_cm_scale, ctx->stream);
     CK(hipGetLastError());
     return BANN_OK;
   }
-  if (!ctx->d_ones) {
-    CK(dalloc(&ctx->d_ones, n));
-    std::vector<float> one((size_t)n, 1.f);
-    CK(hipMemcpy(ctx->d_ones, one.data(), n * sizeof(float), hipMemcpyHostToDevice));
-    CK(dalloc(&ctx->d_cm, ((int64_t)ctx->br.size() + 1) * 2 * CM_NC));
-  }
+  if (ctx->total_p > (int64_t(1) << 31))  // the per-bin u64 fixed-point r sums (k_cm_hist, CM_FIX)
+    return fail(ctx, BANN_E_SHAPE, "common-mode rule: more than 2^31 parameters on one rank");
+  if (ctx->cm_rule == 3) ++ctx->cm_adapted;
   if (!fx_only) {  // every branch's target f_b - 1 (the prediction rows at theta_0 first)
     int rc = run_forward(ctx, p);
     if (rc) return rc;
     launch_net_targets(ctx->st, p.d_all, nb, ctx->d_ones, nullptr, 0.f, nullptr, nullptr, ctx->stream);
   }
   ctx->st.nete = fx_only ? ctx->d_ones : nullptr;
-  int rc = run_grad(ctx, p, 0);
+  rc = run_grad(ctx, p, 0);
   ctx->st.nete = fx_only ? ctx->d_netsum : nullptr;
   if (rc) return rc;
   const double T = (double)ctx->cm_tau * ctx->cm_tau * (double)n / (double)lambda_e;
@@ -245,9 +293,9 @@ int common_mode_steps(bann_ctx* ctx, const Plan& p, bool fx_only, float lambda_e
   rc = allreduce_host_f64(ctx, h.data(), 2 * CM_NC);  // over ranks: every rank picks the same t
   if (rc) return rc;
   // f_k / T = 2^(-k/2) #{r >= 2^(-k/2)} + sum_{r < 2^(-k/2)} r, in bins (bin j >= 1 holds
-  // 2^(-j/2) <= r < 2^(-(j-1)/2); its r sum in units of 2^-38)
+  // 2^(-j/2) <= r < 2^(-(j-1)/2); its r sum in units of 2^-CM_FIX_LOG2)
   std::vector<double> tail(CM_NC + 1, 0.0);  // tail[k] = sum of r over bins > k
-  for (int k = CM_NC - 1; k >= 1; --k) tail[k - 1] = tail[k] + h[CM_NC + k] * 0x1p-38;
+  for (int k = CM_NC - 1; k >= 1; --k) tail[k - 1] = tail[k] + std::ldexp(h[CM_NC + k], -CM_FIX_LOG2);
   double total = 0.0;
   for (int k = 0; k < CM_NC; ++k) total += h[k];
   double cnt = 0.0;
@@ -292,14 +340,14 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
   if (!y || L < 1) return fail(ctx, BANN_E_ARG, "null targets or L < 1");
   if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
-  if (step_mode != BANN_STEP_IZMAILOV && step_mode != BANN_STEP_UNIFORM && step_mode != BANN_STEP_INJECTED)
-    return fail(ctx, BANN_E_ARG, "network mode: Izmailov, uniform or injected step sizes");
+  if (step_mode != BANN_STEP_IZMAILOV && step_mode != BANN_STEP_UNIFORM && step_mode != BANN_STEP_STD_SCALED &&
+      step_mode != BANN_STEP_INJECTED)
+    return fail(ctx, BANN_E_ARG, "network mode: Izmailov, uniform, StdScaled or injected step sizes");
   const int64_t n = ctx->n;
   const int32_t nb = (int32_t)ctx->br.size();
-  if (!ctx->d_netsum) {
-    CK(dalloc(&ctx->d_netsum, n));
-    CK(dalloc(&ctx->d_nety, n));
-    CK(dalloc(&ctx->d_netpart, net_scratch_doubles(n)));
+  {
+    int rc0 = net_buffers_init(ctx);  // allocated at bann_finalize: a no-op here
+    if (rc0) return rc0;
   }
   if (ctx->netrss_cap < L + 1) {
     dfree(ctx->d_netrss);
@@ -432,9 +480,12 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   }
   mark_predictions(ctx, p, true);
   CK(hipGetLastError());
+  double rss_final = rss[L];
+  if (status != BANN_ACCEPTED)  // theta_0's rss, recomputed into d_netrss[L] after the restore above
+    CK(hipMemcpyAsync(&rss_final, ctx->d_netrss + L, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   CK(hipStreamSynchronize(ctx->stream));
   if (status_out) *status_out = status;
   if (h_trace_out) std::copy(H.begin(), H.begin() + L + 1, h_trace_out);  // H[L + 1] is the shared uniform
-  if (rss_out) *rss_out = rss[L];
+  if (rss_out) *rss_out = rss_final;
   return BANN_OK;
 }

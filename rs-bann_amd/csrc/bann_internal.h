@@ -199,8 +199,10 @@ int64_t net_scratch_doubles(int64_t n);
 // common-mode step sizes of the network-joint state (kernels_update.hip): per branch the common-mode
 // gains a_p = eps_p |g_p| (g: the branch's partial slabs after a gradient launch with output error 1)
 // into st.grad and a histogram of a_p^2 / T (part: nb x 2 CM_NC, out: 2 CM_NC = counts, then
-// fixed-point sums in units of 2^-38); then eps_p *= min(1, t / a_p)
+// fixed-point sums in units of 2^-32: no wrap below 2^32 parameters per bin); then eps_p *= min(1, t / a_p)
 #define CM_NC 96
+#define CM_FIX_LOG2 32
+void launch_fill_f32(float* p, float v, int64_t n, hipStream_t s);
 void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, float inv_T, unsigned long long* part,
                     unsigned long long* out, hipStream_t s);
 void launch_cm_apply(const DevState& st, const int32_t* branches, int32_t nb, int32_t max_p, float t, float* scale,
@@ -226,7 +228,7 @@ void launch_forward_fi(const DevState& st, const GradItem* items, int32_t nitems
 void launch_pack_fi(const uint8_t* raw, int64_t rowb, const PackJob* jobs, int32_t njobs, const int32_t* idx,
                     int64_t ntile, uint8_t* dst, hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                           int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s);
+                           int32_t nw, int32_t cpw, int full, int write_pred, int head, hipStream_t s);
 int fxl_lds_bytes(int nw, int nl, int cpw);
 int fxl_cpw(int nchunks);  // marker chunks per fxl wave: 4 up to 32 chunks, else 8
 void launch_step_sizes(const DevState& st, const double* base, const int32_t* branches, int32_t nb, int32_t max_p,

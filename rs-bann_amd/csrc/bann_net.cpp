@@ -977,8 +977,18 @@ int train_begin(bann_net* t, const float* y, int64_t n, const bann_mcmc_cfg* cfg
   if (cfg->hmc_integration_length < 1 || cfg->chain_length < 0 || cfg->burn_in < 0)
     return fail(t, BANN_E_ARG, "bad MCMC configuration");
   const int32_t m = cfg->hmc_step_size_mode;
-  if (!cfg->joint_hmc && m != BANN_STEP_IZMAILOV && m != BANN_STEP_UNIFORM && m != BANN_STEP_RANDOM)
-    return fail(t, BANN_E_ARG, "step size mode: Izmailov, uniform or random (StdScaled is unusable in the reference)");
+  if (!cfg->joint_hmc && m != BANN_STEP_IZMAILOV && m != BANN_STEP_UNIFORM && m != BANN_STEP_RANDOM &&
+      m != BANN_STEP_STD_SCALED)
+    return fail(t, BANN_E_ARG, "step size mode: Izmailov, uniform, random or StdScaled");
+  // StdScaled returns empty step sizes for the ARD priors (ridge_ard.rs:56-68, lasso_ard.rs:62-74):
+  // the reference's hmc_step would index-panic on the first half step; joint HMC uses random
+  // sizes instead (branch_sampler.rs:1092-1101)
+  if (!cfg->joint_hmc && !cfg->gradient_descent && !cfg->gradient_descent_joint && m == BANN_STEP_STD_SCALED)
+    for (const auto& B : t->br)
+      if (is_ard(B.prior))
+        return fail(t, BANN_E_ARG,
+                    "StdScaled step sizes are empty for the ARD priors in the reference (ridge_ard.rs:56-68, "
+                    "lasso_ard.rs:62-74): use Izmailov, uniform or random");
   if (n != bann_ctx_num_individuals(t->ctx)) return fail(t, BANN_E_SHAPE, "phenotype length differs from the cohort");
   t->n = n;
   // net.rs:208-211: the models and effect-size directories

@@ -28,6 +28,7 @@ struct LaunchGroup {
   int32_t kind = 0;  // BranchDev::fused of its branches: 1 fx, 3 fxl, 2 wx
   int32_t L = 0, act = 0, nw = 1, full = 0;
   int32_t cpw = 8;      // fxl: marker chunks per wave (fxl_cpw)
+  int32_t head = 0;     // fxl: the head-wave kernel fxh where its shape allows (bann_ctx::fxl_head)
   int64_t tiles = 0;    // fx: the items' 64-individual tiles (the fi forward's index space, GradItem::tile0)
   int32_t max_seg = 1;  // fx: the largest 256-marker segment count of its branches
   bool fi = false;      // fx: every branch has an individual-major fi image (kernels_fi.hip)
@@ -78,7 +79,8 @@ struct bann_ctx {
   std::vector<BranchHost> br;
   bool finalized = false;
   bool fused_enabled = true;
-  bool wide_bf16 = false;  // wx kernel: hidden GEMMs on bf16 MFMA (opt-in, reduced precision)
+  bool wide_bf16 = false;
+  bool fxl_head = true;    // fxl groups of 17..32 chunks on the head-wave kernel (BANN_FXL_HEAD=0 at creation: off)  // wx kernel: hidden GEMMs on bf16 MFMA (opt-in, reduced precision)
   int32_t nfrag = 0, max_splits = 1;
   int64_t packed_bytes = 0, total_p = 0;
   // device buffers
@@ -140,7 +142,10 @@ struct bann_ctx {
   double* d_netpart = nullptr; // network mode: rss block partials
   int32_t netrss_cap = 0;
   // network mode: the common-mode step-size rule (bann_set_network_step_rule)
-  int32_t cm_rule = 1;           // 0 off, 1 adapt before every trajectory, 2 frozen (bann_set_network_step_rule)
+  // 0 off, 1 adapt before every trajectory (diagnostic: state-dependent proposals), 2 frozen,
+  // 3 auto (default): adapt on the first cm_adapt_total trajectories, then frozen
+  int32_t cm_rule = 3;
+  int32_t cm_adapt_total = 1, cm_adapted = 0;  // auto mode: adapting trajectories asked / done
   float* d_cm_scale = nullptr;    // the last adapted per-parameter step factors
   bool cm_have_scale = false;
   float cm_tau = 1.0f;
@@ -243,3 +248,6 @@ enum { TM_GRAD0 = 0, TM_GRAD1 = 1, TM_UPD1 = 2, TM_AR0 = 3, TM_AR1 = 4, TM_FWD0 
 void tm_mark(bann_ctx* ctx, int32_t kind);
 void tm_mark_follow(bann_ctx* ctx, int32_t kind);
 int tm_resolve(bann_ctx* ctx);  // after the stream has drained
+// bann_dist.hip: the network sampler's device buffers, allocated once at bann_finalize
+// (no allocation or synchronous upload inside a collective trajectory)
+int net_buffers_init(bann_ctx* ctx);

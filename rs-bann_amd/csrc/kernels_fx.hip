@@ -1600,14 +1600,14 @@ int fxl_cpw(int nchunks) {
 
 // nw waves per workgroup (= ceil(chunks / cpw) of every branch of the launch);
 // full: every branch has exactly cpw * nw chunks
-bool fxh_takes(int nw, int cpw);
+bool fxh_takes(int nw, int cpw, int head);
 template <int NL>
 static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nitems, int act, int nc, int wp,
                           int slot_kib, hipStream_t s);
 void launch_fused_grad_fxl(const DevState& st, const GradItem* items, int32_t nitems, int32_t L, int32_t act,
-                           int32_t nw, int32_t cpw, int full, int write_pred, hipStream_t s) {
+                           int32_t nw, int32_t cpw, int full, int write_pred, int head, hipStream_t s) {
   if (nitems <= 0 || nw < 1 || nw > FXL_MAXW || (cpw != 4 && cpw != 8)) return;
-  if (fxh_takes(nw, cpw) && L >= 2 && L <= 4) {  // the head-wave kernel: ceil(4 nw / 5) compute waves
+  if (fxh_takes(nw, cpw, head) && L >= 2 && L <= 4) {  // the head-wave kernel: ceil(4 nw / 5) compute waves
     const int nc = (4 * nw + FXH_CPW - 1) / FXH_CPW;
     if (L == 2) launch_fxh_nl<2>(st, items, nitems, act, nc, write_pred, FXH_CPW, s);
     if (L == 3) launch_fxh_nl<3>(st, items, nitems, act, nc, write_pred, FXH_CPW, s);
@@ -2080,8 +2080,6 @@ static void launch_fxh_nl(const DevState& st, const GradItem* items, int32_t nit
 }
 
 // the head-wave kernel for fxl groups of 4-chunk waves with >= 5 waves (17 .. 32
-// chunks); BANN_FXL_HEAD=0 keeps fxl (A/B)
-bool fxh_takes(int nw, int cpw) {
-  const char* e = getenv("BANN_FXL_HEAD");  // read per launch: tests switch it between contexts
-  return (!e || atoi(e) != 0) && cpw == 4 && nw >= 5 && nw <= 8;
-}
+// chunks); head = the context's choice (bann_ctx::fxl_head, read once at context
+// creation: BANN_FXL_HEAD=0 keeps fxl for A/B), part of the launch group and its graph key
+bool fxh_takes(int nw, int cpw, int head) { return head && cpw == 4 && nw >= 5 && nw <= 8; }

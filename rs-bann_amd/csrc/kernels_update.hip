@@ -833,7 +833,9 @@ void launch_sample_momentum_joint(const DevState& st, const int32_t* branches, i
 // t_k^2 = T 2^(-k/2) from a histogram of r_p = a_p^2 / T (integer counts and fixed-point sums:
 // deterministic), summed over branches and ranks.
 // bin 0: r >= 1; bin j (1 <= j < CM_NC - 1): 2^(-j/2) <= r < 2^(-(j-1)/2); last bin: smaller
-#define CM_FIX 0x1p38  // fixed-point unit of the r sums (bins >= 1: r < 1, <= 2^25 params per bin)
+// fixed-point unit of the r sums: bins >= 1 hold r < 1, so a u64 bin sum cannot wrap below 2^32
+// parameters (bann_dist.hip refuses more than 2^31 per rank)
+#define CM_FIX ((double)(1ull << CM_FIX_LOG2))
 __device__ __forceinline__ int cm_bin(float r) {
   if (!(r < 1.f)) return 0;
   if (!(r > 0.f)) return CM_NC - 1;
@@ -896,6 +898,15 @@ __global__ void __launch_bounds__(256) k_cm_rescale(DevState st, const int32_t* 
     const float f = scale[bd.p_off + i];
     if (f < 1.f) st.eps[bd.p_off + i] *= f;
   }
+}
+
+__global__ void __launch_bounds__(256) k_fill_f32(float* __restrict__ p, float v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+void launch_fill_f32(float* p, float v, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fill_f32, dim3(g), dim3(256), 0, s, p, v, n);
 }
 
 void launch_cm_hist(const DevState& st, const int32_t* branches, int32_t nb, float inv_T, unsigned long long* part,

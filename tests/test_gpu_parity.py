@@ -371,6 +371,65 @@ def test_device_step_sizes_match_oracle(Ctx, mode):
     ctx.close()
 
 
+def test_std_scaled_step_sizes_match_oracle(Ctx):
+    """StepSizeMode::StdScaled (branch_sampler.rs:1213): c * sqrt(1 / lambda_l) per weight
+    layer and c * (1 / sqrt(lambda_b)) per bias for RidgeBase / LassoBase / StdNormal
+    (ridge_base.rs:52-82, lasso_base.rs:53-82, std_normal_branch.rs:51-80) equal the oracle's
+    f32 restatement to 2e-7; the ARD priors, whose reference vectors are empty
+    (ridge_ard.rs:56-68, lasso_ard.rs:62-74), are refused."""
+    from bann import BannError
+    rng = np.random.default_rng(32)
+    n, m = 128, 40
+    priors = ["ridge_base", "lasso_base", "std_normal", "ridge_ard", "lasso_ard"]
+    g = O.synthetic_genotypes(rng, n, m * len(priors))
+    specs = [dict(snps=np.arange(k * m, (k + 1) * m, dtype=np.int32),
+                  branch=f32_branch(O.random_branch(rng, m, [4, 3, 1], prior=p)), y=rng.normal(size=n))
+             for k, p in enumerate(priors)]
+    ctx = build_context(Ctx, g, specs)
+    L, c = 7, 0.37
+    ctx.leapfrog_begin([0, 1, 2], L, 10.0, "std_scaled", c, seed=1)
+    ctx.leapfrog_end()
+    for k in range(3):
+        got = ctx.get_step_sizes(k)
+        ref = O.param_vec(*O.std_scaled_step_sizes(specs[k]["branch"], c)).astype(np.float32)
+        assert np.allclose(got, ref, rtol=2e-7, atol=0), (priors[k], np.max(np.abs(got / ref - 1)))
+    for k in (3, 4):
+        with pytest.raises(BannError, match="ARD"):
+            ctx.hmc_step([k], L, 10.0, step_mode="std_scaled", step_factor=c, seed=2)
+        with pytest.raises(ValueError):
+            O.std_scaled_step_sizes(specs[k]["branch"], c)
+    ctx.close()
+
+
+@pytest.mark.parametrize("prior", ["ridge_base", "lasso_base", "std_normal"])
+def test_hmc_step_std_scaled_matches_oracle(Ctx, prior):
+    """A whole hmc_step trajectory in StdScaled mode (the step sizes formed by the library,
+    momentum and uniform injected) reproduces the oracle's -H trace, status and end state."""
+    rng = np.random.default_rng(33)
+    n, m, L, c = 400, 96, 8, 0.02
+    g = O.synthetic_genotypes(rng, n, m)
+    br = f32_branch(O.random_branch(rng, m, [4, 4, 1], prior=prior))
+    ctx = build_context(Ctx, g, [dict(snps=np.arange(m, dtype=np.int32), branch=br, y=np.zeros(n))])
+    mu, sd = ctx.genotype_stats()
+    X = x_std(g, mu, sd)
+    y = (O.predict(br, X) + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    ctx.set_target(0, y)
+    p0 = rng.normal(size=br.num_params).astype(np.float32)
+    res = ctx.hmc_step([0], L, 10.0, step_mode="std_scaled", step_factor=c, momentum=p0, u=[0.5])
+    ew, eb = O.std_scaled_step_sizes(br, c)
+    ew = [e.astype(np.float64) for e in ew]
+    eb = [e.astype(np.float64) for e in eb]
+    pw, pb = O.load_param_vec(p0.astype(np.float64), m, br.layer_widths)
+    ob_ = br.copy()
+    out = O.hmc_step(ob_, X, y, ew, eb, pw, pb, L, 10.0, 0.5)
+    assert res["status"][0] == out["status"]
+    tr = np.asarray(out["trace"])
+    gt = res["trace"][0][: tr.size]
+    assert np.all(np.abs(gt - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (gt, tr)
+    assert norm_rel(ctx.get_params(0), O.param_vec(ob_.weights, ob_.biases)) < 1e-5
+    ctx.close()
+
+
 def test_device_momentum_moments(Ctx):
     """k_sample_momentum (sample_momentum, branch_sampler.rs:594-609: p ~ N(0, 1)):
     the device momenta are recovered from the first recorded position step of a

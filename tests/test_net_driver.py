@@ -63,6 +63,9 @@ def rel(a, b):
     ("ridge_ard", dict(joint_hmc=True, factor=0.5)), ("lasso_base", dict(joint_hmc=True, factor=0.5)),
     # StepSizeMode::Random (branch_sampler.rs:654-681, 1212-1217)
     ("ridge_base", dict(step_mode="random")),
+    # StepSizeMode::StdScaled (ridge_base.rs:52-82, lasso_base.rs:53-82, dispatched at 1213)
+    ("ridge_base", dict(step_mode="std_scaled", factor=0.05)),
+    ("lasso_base", dict(step_mode="std_scaled", factor=0.05, sampled_output_bias=True)),
     # Net::train_single_branch (net.rs:360-507)
     ("ridge_ard", dict(single_branch=True)),
     # MCMCCfg::gradient_descent (line search over rss probes, branch_sampler.rs:964-1016)
@@ -171,6 +174,19 @@ def test_model_file_roundtrip(tmp_path):
         net3.load(str(tmp_path / "models" / "3.bin"))
     for o in (net, net2, net3, ctx, ctx2, ctx3):
         o.close()
+
+
+def test_std_scaled_refused_for_ard():
+    """StdScaled returns empty step sizes for the ARD priors (ridge_ard.rs:56-68,
+    lasso_ard.rs:62-74) -- the reference's hmc_step would index-panic: the driver refuses
+    the configuration before the first sweep."""
+    from bann import BannError, MCMCConfig, Net
+    ctx, branches, X, y = build("ridge_ard")
+    net = Net(ctx, seed=3)
+    with pytest.raises(BannError, match="ARD"):
+        net.train(y, MCMCConfig(hmc_integration_length=5, chain_length=1, hmc_step_size_mode="std_scaled"))
+    net.close()
+    ctx.close()
 
 
 def test_std_normal_cannot_train():

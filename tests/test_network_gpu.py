@@ -384,3 +384,82 @@ def test_common_mode_rule_frozen():
         for b in range(len(specs)):
             assert np.array_equal(ctx.get_step_sizes(b), eps_a[b]), b
     ctx.close()
+
+
+def _fx_network(seed=13, n=1500, nbr=8):
+    rng = np.random.default_rng(seed)
+    shapes = [(60, [4, 4, 1], "ridge_ard")] * nbr
+    M = sum(m for m, _, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w, prior in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior=prior))))
+        off += m
+    ctx = _context(g, specs, range(len(specs)))
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    y = (sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+         + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    return rng, ctx, specs, Xs, y
+
+
+def test_common_mode_rule_default_is_state_independent():
+    """A caller who never calls bann_set_network_step_rule gets the auto rule (mode 3): the
+    first trajectory adapts the common-mode factors (burn-in), every later one applies them
+    frozen -- step sizes that depend on the precisions only, not on the trajectory's start
+    theta_0, as HMC's detailed balance needs.  Checked by restarting from a different theta_0
+    (set_params): the frozen steps are bit for bit the same; the adaptive diagnostic mode (1)
+    would change them (so the check can tell the two apart)."""
+    rng, ctx, specs, Xs, y = _fx_network()
+    L, c, le = 6, 1.0, 2.0
+    st = ctx.network_step_rule_state()
+    assert st == dict(mode="auto", adapted=0, frozen=False), st
+    ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=5)
+    assert np.isfinite(ctx.network_step_rule_info()["threshold"])  # the rule scaled some steps
+    st = ctx.network_step_rule_state()
+    assert st["adapted"] == 1 and st["frozen"], st
+    eps_a = [ctx.get_step_sizes(b).copy() for b in range(len(specs))]
+    theta_other = []
+    for b, s in enumerate(specs):  # a very different start: every parameter scaled and shifted
+        th = O.param_vec(s["branch"].weights, s["branch"].biases)
+        theta_other.append((1.7 * th + 0.05 * rng.normal(size=th.size)).astype(np.float32))
+    for seed in (6, 7):
+        for b, th in enumerate(theta_other):
+            ctx.set_params(b, th)
+        ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=seed)
+        for b in range(len(specs)):
+            assert np.array_equal(ctx.get_step_sizes(b), eps_a[b]), (seed, b)
+    # the diagnostic mode re-adapts from the new theta_0: different steps
+    ctx.set_network_step_rule("adaptive")
+    for b, th in enumerate(theta_other):
+        ctx.set_params(b, th)
+    ctx.network_hmc_step(y, L, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=8)
+    assert any(not np.array_equal(ctx.get_step_sizes(b), eps_a[b]) for b in range(len(specs)))
+    # auto again with K = 2 adapting trajectories
+    ctx.set_network_step_rule("auto")
+    ctx.set_network_adapt_trajectories(2)
+    for k in range(3):
+        assert ctx.network_step_rule_state()["frozen"] == (k == 2)
+        ctx.network_hmc_step(y, 2, bias=0.1, lambda_e=le, step_mode="izmailov", step_factor=c, seed=20 + k)
+    ctx.close()
+
+
+def test_network_rss_out_on_rejection():
+    """bann_network_hmc_step's rss output is the final state's: theta_L when accepted,
+    theta_0 (the restored state) when rejected -- checked on a forced early rejection
+    against the oracle rss of the starting state."""
+    rng, ctx, specs, Xs, y = _fx_network(seed=17, nbr=4)
+    ctx.set_network_step_rule("off")
+    bias = 0.1
+    f0 = sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+    rss0 = float(np.sum((y - bias - f0) ** 2))
+    eps = np.concatenate([np.full(s["branch"].num_params, 0.5, np.float32) for s in specs])  # absurd steps
+    mom = np.concatenate([rng.normal(size=s["branch"].num_params).astype(np.float32) for s in specs])
+    res = ctx.network_hmc_step(y, 4, bias=bias, lambda_e=2.0, max_hamiltonian_error=1e-3, eps=eps, momentum=mom,
+                               u=0.5)
+    assert res["status"] == 2, res["status"]
+    assert abs(res["rss"] - rss0) <= 1e-5 * max(1.0, rss0), (res["rss"], rss0)
+    for b, s in enumerate(specs):
+        assert np.array_equal(ctx.get_params(b), O.param_vec(s["branch"].weights, s["branch"].biases).astype(np.float32))
+    ctx.close()
