@@ -442,6 +442,10 @@ int bann_set_network_adapt_trajectories(bann_ctx* ctx, int32_t k);
 /* the rule's state: mode, adapting trajectories done in auto mode, and whether the NEXT
  * trajectory applies frozen factors (1) or adapts / runs without the rule (0) */
 int bann_network_step_rule_state(const bann_ctx* ctx, int32_t* mode, int32_t* adapted, int32_t* frozen);
+/* the network sampler's forward: the group-sum rows of its plan (k_forward_gsum: every
+ * branch an fx branch of 8 chunks -- each step's forward but the last writes one row per
+ * group of four branches), 0 = per-branch output rows, -1 = no network trajectory yet */
+int bann_network_info(const bann_ctx* ctx, int32_t* group_rows);
 /* the last network trajectory's rule: [threshold t (inf: no step changed),
  * (omega eps)^2 of the common mode before (inf when some single parameter alone
  * exceeded tau) and after, the fraction of parameters whose step was reduced] */

@@ -135,6 +135,7 @@ SIGNATURES = {
     "bann_set_network_step_rule": (C.c_int, [_P, _i32, _f32]),
     "bann_network_step_rule_info": (C.c_int, [_P, _pf64]),
     "bann_set_network_adapt_trajectories": (C.c_int, [_P, _i32]),
+    "bann_network_info": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "bann_network_step_rule_state": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "bann_residual_set": (C.c_int, [_P, _pf32]),
     "bann_residual_get": (C.c_int, [_P, _pf32]),

@@ -459,6 +459,12 @@ class BannContext:
         return dict(mode={0: "off", 1: "adaptive", 2: "frozen", 3: "auto"}[m.value], adapted=a.value,
                     frozen=bool(f.value))
 
+    def network_group_rows(self) -> int:
+        """the network forward's group-sum rows (k_forward_gsum), 0: per-branch rows, -1: not run yet"""
+        r = C.c_int32()
+        self._check(self._lib.bann_network_info(self._h, C.byref(r)))
+        return r.value
+
     def network_step_rule_info(self) -> dict:
         """the last network trajectory's rule: threshold t, (omega eps)^2 of the common mode
         before and after, the fraction of parameters whose step was reduced."""

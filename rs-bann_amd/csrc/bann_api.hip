@@ -31,7 +31,10 @@ void free_plan(Plan& p) {
     dfree(p.d_gx);
     dfree(p.d_gxpre);
     dfree(p.d_fold);
-    for (auto& g : p.groups) dfree(g.d_items);
+    for (auto& g : p.groups) {
+      dfree(g.d_items);
+      dfree(g.d_nitems);
+    }
   }
   p = Plan{};
 }
@@ -504,6 +507,8 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   ctx->device = device;
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
   if (const char* e = getenv("BANN_FXL_HEAD")) ctx->fxl_head = atoi(e) != 0;
+  if (const char* e = getenv("BANN_NET_GSUM")) ctx->net_gsum = atoi(e) != 0;
+  if (const char* e = getenv("BANN_NET_GW")) ctx->net_gw = atoi(e) == 4 ? 4 : 8;
   if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -533,7 +538,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
                   ctx->d_plan_scr, ctx->d_gen_scr, ctx->d_gxpre_scr, ctx->d_delta, ctx->d_delta_part, ctx->d_stepbase,
                   ctx->d_phi, ctx->d_phi0, ctx->d_mphi, ctx->d_ephi, ctx->d_gphi, ctx->d_pidx, ctx->d_ows,
                   ctx->d_netsum, ctx->d_nety, ctx->d_netrss, ctx->d_netpart, ctx->d_ar64, ctx->d_res, ctx->d_upd_cnt,
-                  ctx->d_res_part, ctx->d_ones, ctx->d_cm, ctx->d_cm_scale};
+                  ctx->d_res_part, ctx->d_ones, ctx->d_cm, ctx->d_cm_scale, ctx->d_gsum};
   for (hipEvent_t e : ctx->tm_pool) (void)hipEventDestroy(e);
   clear_graphs(ctx);
   comm_destroy(ctx);

@@ -237,6 +237,23 @@ int net_buffers_init(bann_ctx* ctx) {
     const BranchHost& last = ctx->br.back();
     CK(dalloc(&ctx->d_cm_scale, last.dev.p_off + last.P));
   }
+  if (!ctx->d_gsum && ctx->net_gsum) {  // one row per group of <= 4 fx branches of 8 chunks and one (L, act)
+    std::vector<std::pair<int64_t, int32_t>> cls;  // ((L, act), count)
+    for (const auto& h : ctx->br)
+      if (h.dev.fused == 1 && h.dev.nchunks == 8) {
+        const int64_t key = (int64_t)h.L * 64 + h.act;
+        bool found = false;
+        for (auto& c : cls)
+          if (c.first == key) ++c.second, found = true;
+        if (!found) cls.push_back({key, 1});
+      }
+    int64_t rows = 0;
+    for (const auto& c : cls) rows += (c.second + 3) / 4;
+    if (rows > 0) {
+      CK(dalloc(&ctx->d_gsum, rows * n));
+      ctx->gsum_cap = (int32_t)rows;
+    }
+  }
   if (!ctx->d_ones) {
     CK(dalloc(&ctx->d_ones, n));
     launch_fill_f32(ctx->d_ones, 1.f, n, ctx->stream);
@@ -246,13 +263,78 @@ int net_buffers_init(bann_ctx* ctx) {
   return BANN_OK;
 }
 
+extern "C" int bann_network_info(const bann_ctx* ctx, int32_t* group_rows) {
+  if (!ctx) return BANN_E_ARG;
+  if (group_rows) *group_rows = ctx->lf.nsum_built ? ctx->lf.nsum_rows : -1;
+  return BANN_OK;
+}
+
 extern "C" int bann_network_step_rule_info(const bann_ctx* ctx, double* out4) {
   if (!ctx || !out4) return BANN_E_ARG;
   for (int k = 0; k < 4; ++k) out4[k] = ctx->cm_info[k];
   return BANN_OK;
 }
 
+// k_forward_gsum's work items for a persistent network plan: usable when every branch of the
+// plan is an fx branch of exactly 8 chunks (the full8 groups), L <= 4.  Each launch group's
+// branches, in plan order, form groups of four (one output row each); every group is split
+// into sp tile ranges with sp chosen as the fx plan's split count is: the fewest rounds of
+// two workgroups per CU times the tiles per wave (+2 for the prologue).
+int build_net_groups(bann_ctx* ctx, Plan& p) {
+  p.nsum_built = true;
+  p.nsum_rows = 0;
+  if (!ctx->d_gsum || !p.gx.empty() || p.groups.empty()) return BANN_OK;
+  for (const auto& g : p.groups)
+    if (g.kind != 1 || !g.full || g.L < 2 || g.L > 4) return BANN_OK;
+  const int64_t ntile = ((int64_t)ctx->nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
+  const int gw = ctx->net_gw;
+  p.nsum_gw = gw;
+  const int64_t slots = (gw == 8 ? 1 : 2) * (int64_t)ctx->cus;  // workgroups per CU (LDS)
+  int32_t row = 0;
+  for (auto& g : p.groups) {
+    std::vector<int32_t> brs;
+    for (const auto& it : g.items)
+      if (brs.empty() || brs.back() != it.branch) brs.push_back(it.branch);
+    const int64_t ng = ((int64_t)brs.size() + gw - 1) / gw;
+    if (row + ng > ctx->gsum_cap) {  // cannot happen: the cap counts every 8-chunk fx branch
+      p.nsum_rows = 0;
+      return BANN_OK;
+    }
+    int64_t best = -1, sp_best = 1;
+    for (int64_t sp = 1; sp <= std::min<int64_t>(ntile, 256); ++sp) {
+      const int64_t cost = ((ng * sp + slots - 1) / slots) * ((ntile + sp - 1) / sp + 2);
+      if (best < 0 || cost < best) best = cost, sp_best = sp;
+    }
+    g.nitems.clear();
+    for (int64_t gi = 0; gi < ng; ++gi)
+      for (int64_t s = 0; s < sp_best; ++s) {
+        NetGroupItem it{};
+        for (int w = 0; w < 8; ++w) it.b[w] = w < gw && gw * gi + w < (int64_t)brs.size() ? brs[gw * gi + w] : -1;
+        it.tile_begin = (int32_t)(ntile * s / sp_best);
+        it.tile_end = (int32_t)(ntile * (s + 1) / sp_best);
+        it.row = row + (int32_t)gi;
+        if (it.tile_end > it.tile_begin) g.nitems.push_back(it);
+      }
+    row += (int32_t)ng;
+    dfree(g.d_nitems);
+    g.d_nitems = nullptr;
+    CK(dalloc(&g.d_nitems, (int64_t)g.nitems.size()));
+    CK(hipMemcpyAsync(g.d_nitems, g.nitems.data(), g.nitems.size() * sizeof(NetGroupItem), hipMemcpyHostToDevice,
+                      ctx->stream));
+  }
+  CK(hipStreamSynchronize(ctx->stream));  // the host item vectors stay, but keep the copy off the timed path
+  p.nsum_rows = row;
+  return BANN_OK;
+}
+
 namespace {
+// the group-sum forward of a plan with build_net_groups items (network mode)
+void run_forward_gsum(bann_ctx* ctx, const Plan& p) {
+  for (const auto& g : p.groups)
+    launch_forward_gsum(ctx->st, g.d_nitems, (int32_t)g.nitems.size(), g.L, g.act, p.nsum_gw, ctx->d_gsum,
+                        ctx->stream);
+}
+
 // the common-mode rule (bann.h bann_set_network_step_rule; kernels_update.hip k_cm_*): one gradient
 // launch with output error 1 gives g = J^T 1 of every local branch, the histogram of
 // r_p = (eps_p g_p)^2 / T is summed over branches and ranks, and eps_p *= min(1, t / (eps_p |g_p|))
@@ -362,6 +444,10 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
     int rc = build_plan(ctx, all.data(), nb, ctx->lf, true);
     if (rc) return rc;
   }
+  if (!ctx->lf.nsum_built) {
+    int rc0 = build_net_groups(ctx, ctx->lf);
+    if (rc0) return rc0;
+  }
   const Plan& p = ctx->lf;
   int rc = traj_prepare(ctx, p, L, max_dh, step_mode, factor, eps, momentum, seed, nullptr);
   if (rc) return rc;
@@ -374,16 +460,33 @@ extern "C" int bann_network_hmc_step(bann_ctx* ctx, const float* y, float bias, 
   if (const char* e = getenv("BANN_NET_ERR"))  // 0: per-branch targets for every kind (diagnostics)
     fx_only = fx_only && atoi(e) != 0;
   ctx->st.nete = fx_only ? ctx->d_netsum : nullptr;
+  // group sums (k_forward_gsum): every step's forward but the last writes one row per group of
+  // four branches instead of every branch's outputs -- the step needs only their sum, and the
+  // per-gradient kernels read e (fx_only).  Step 0 too when every prediction row is already
+  // f_b(theta_0) (the snapshot into pred0 below copies them); the last step's forward writes
+  // the per-branch rows the final targets and the residual need.
+  const bool gsum = fx_only && p.nsum_rows > 0;
+  bool rows_current = true;
+  for (int32_t b : p.all) rows_current = rows_current && ctx->pred_ok[b];
   // f_b at the current theta -> sum over branches and ranks -> e -> targets y_b = f_b - e -> gradients
   // (launch timing, when enabled: forward, all-reduce, gradient and update spans)
   auto forward_and_targets = [&](int k) -> int {
     tm_mark_follow(ctx, TM_FWD0);  // the previous step's update end
-    int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
-    if (r) return r;
+    const bool grp = gsum && k < L && (k > 0 || rows_current);
+    if (grp) {
+      run_forward_gsum(ctx, p);
+      CK(hipGetLastError());
+    } else {
+      int r = run_forward(ctx, p);  // forward-only: the outputs the all-reduce needs
+      if (r) return r;
+    }
     tm_mark(ctx, TM_FWD1);
-    launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
+    if (grp)
+      launch_net_sum_rows(ctx->st, ctx->d_gsum, p.nsum_rows, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
+    else
+      launch_net_sum(ctx->st, p.d_all, nb, ctx->d_netsum, ctx->d_delta_part, ctx->stream);
     tm_mark(ctx, TM_AR0);
-    r = allreduce_device_f32(ctx, ctx->d_netsum, n);
+    int r = allreduce_device_f32(ctx, ctx->d_netsum, n);
     if (r) return r;
     tm_mark(ctx, TM_AR1);
     launch_net_targets(ctx->st, p.d_all, fx_only ? 0 : nb, ctx->d_netsum, ctx->d_nety, bias, ctx->d_netpart,

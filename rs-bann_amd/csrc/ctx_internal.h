@@ -34,6 +34,9 @@ struct LaunchGroup {
   bool fi = false;      // fx: every branch has an individual-major fi image (kernels_fi.hip)
   std::vector<GradItem> items;
   GradItem* d_items = nullptr;
+  // network mode, fx groups of 8-chunk branches: k_forward_gsum's group items (build_net_groups)
+  std::vector<NetGroupItem> nitems;
+  NetGroupItem* d_nitems = nullptr;
 };
 
 // gx path (kernels_gx.hip): the GEMM phases of one scratch group, each over a
@@ -63,6 +66,11 @@ struct Plan {
   // work items, no solo re-split: the leapfrog session runs the update in the
   // gradient launch's tail (kernels_fx.hip, BANN_FUSE_UPDATE=0: separate launches)
   bool fuse_update = false;
+  // network mode: the forward writes group sums (k_forward_gsum) into nsum_rows rows of
+  // bann_ctx::d_gsum (build_net_groups; nsum_built: tried, nsum_rows > 0: usable)
+  bool nsum_built = false;
+  int32_t nsum_rows = 0;
+  int32_t nsum_gw = 8;  // branches per group (waves per workgroup of k_forward_gsum)
 };
 
 struct bann_ctx {
@@ -136,6 +144,10 @@ struct bann_ctx {
   void* nccl = nullptr;   // ncclComm_t
   bann_allreduce_fn ar_fn = nullptr;
   void* ar_user = nullptr;
+  float* d_gsum = nullptr;     // network mode: per-group output sums of the fx branches (gsum_cap rows of n)
+  int32_t gsum_cap = 0;
+  bool net_gsum = true;        // BANN_NET_GSUM=0 at creation: per-branch output rows in every step (A/B)
+  int32_t net_gw = 8;          // branches per group of the group-sum forward (BANN_NET_GW=4: four)
   float* d_netsum = nullptr;   // network mode: n-vector sum of the local branch outputs, then the error e
   float* d_nety = nullptr;     // network mode: the targets y
   double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)
@@ -251,3 +263,5 @@ int tm_resolve(bann_ctx* ctx);  // after the stream has drained
 // bann_dist.hip: the network sampler's device buffers, allocated once at bann_finalize
 // (no allocation or synchronous upload inside a collective trajectory)
 int net_buffers_init(bann_ctx* ctx);
+// network mode: k_forward_gsum's items for a persistent fx-only plan of 8-chunk branches
+int build_net_groups(bann_ctx* ctx, Plan& p);

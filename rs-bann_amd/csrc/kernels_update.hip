@@ -461,6 +461,45 @@ void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, flo
   hipLaunchKernelGGL(k_residual_delta_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, scratch, st.n, out);
 }
 
+// the same over contiguous rows (group sums of k_forward_gsum): RD_GROUPS row slices, then in order
+__global__ void __launch_bounds__(256) k_net_sum_rows_part(const float* __restrict__ rows, int nrows, int64_t n,
+                                                           float* __restrict__ part) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  const int g = blockIdx.y;
+  const int q0 = (int)((int64_t)nrows * g / RD_GROUPS), q1 = (int)((int64_t)nrows * (g + 1) / RD_GROUPS);
+  const bool full = i0 + 4 <= n && (n & 3) == 0;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 8
+  for (int q = q0; q < q1; ++q) {
+    const int64_t o = (int64_t)q * n + i0;
+    if (full) {
+      const float4 p = *reinterpret_cast<const float4*>(rows + o);
+      a0 += p.x;
+      a1 += p.y;
+      a2 += p.z;
+      a3 += p.w;
+    } else {
+      a0 += rows[o];
+      if (i0 + 1 < n) a1 += rows[o + 1];
+      if (i0 + 2 < n) a2 += rows[o + 2];
+      if (i0 + 3 < n) a3 += rows[o + 3];
+    }
+  }
+  float* row = part + (int64_t)g * n + i0;
+  row[0] = a0;
+  if (i0 + 1 < n) row[1] = a1;
+  if (i0 + 2 < n) row[2] = a2;
+  if (i0 + 3 < n) row[3] = a3;
+}
+
+void launch_net_sum_rows(const DevState& st, const float* rows, int32_t nrows, float* out, float* scratch,
+                         hipStream_t s) {
+  const unsigned gx = (unsigned)((st.n + 1023) / 1024);
+  hipLaunchKernelGGL(k_net_sum_rows_part, dim3(gx, RD_GROUPS), dim3(256), 0, s, rows, nrows, st.n, scratch);
+  hipLaunchKernelGGL(k_residual_delta_sum, dim3((unsigned)((st.n + 255) / 256)), dim3(256), 0, s, scratch, st.n, out);
+}
+
 // e = sum f + bias - y (the network's output error, every branch's output
 // gradient), in place of the sum; each branch's target becomes y_b = f_b - e so
 // that the per-branch gradient kernels see e as their error; rss = sum e^2

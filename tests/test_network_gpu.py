@@ -463,3 +463,48 @@ def test_network_rss_out_on_rejection():
     for b, s in enumerate(specs):
         assert np.array_equal(ctx.get_params(b), O.param_vec(s["branch"].weights, s["branch"].biases).astype(np.float32))
     ctx.close()
+
+
+@pytest.mark.parametrize("gsum", ["1", "0"])
+def test_network_group_sum_forward(monkeypatch, gsum):
+    """k_forward_gsum (the network forward of 8-chunk fx branches): every step's forward but
+    the last sums groups of four branches in LDS and writes one row per group.  Six branches
+    (a full group and a half one), an odd n (a partial last tile and a single-float row tail),
+    two trajectories (the second starts from current prediction rows, so its step 0 is a
+    group forward too): -H trace, status, parameters and the final targets match the oracle,
+    and the per-branch forward (BANN_NET_GSUM=0) agrees."""
+    monkeypatch.setenv("BANN_NET_GSUM", gsum)
+    rng = np.random.default_rng(37)
+    n = 3001
+    shapes = [(500, [4, 4, 1])] * 5 + [(450, [4, 4, 1])]
+    M = sum(m for m, _ in shapes)
+    g = O.synthetic_genotypes(rng, n, M)
+    specs, off = [], 0
+    for m, w in shapes:
+        specs.append(dict(snps=np.arange(off, off + m, dtype=np.int32),
+                          branch=f32_branch(O.random_branch(rng, m, w, prior="ridge_ard"))))
+        off += m
+    ctx = _context(g, specs, range(len(specs)))
+    assert ctx.network_group_rows() == -1
+    mu, sd = ctx.genotype_stats()
+    Xs = [x_std(g[s["snps"]], mu[s["snps"]], sd[s["snps"]]) for s in specs]
+    y = (sum(O.predict(s["branch"], X) for s, X in zip(specs, Xs))
+         + rng.normal(scale=0.5, size=n)).astype(np.float32).astype(np.float64)
+    L = 6
+    for u in (0.3, 0.9):
+        eps, mom = _draws(rng, specs, L)
+        res = ctx.network_hmc_step(y, L, bias=0.1, lambda_e=2.0, eps=np.concatenate(eps),
+                                   momentum=np.concatenate(mom), u=u)
+        assert ctx.network_group_rows() == (2 if gsum == "1" else 0)
+        brs = [s["branch"].copy() for s in specs]
+        out = O.network_hmc_step(brs, Xs, y, 0.1, 2.0, [e.astype(np.float64) for e in eps],
+                                 [p.astype(np.float64) for p in mom], L, 10.0, u)
+        assert res["status"] == out["status"], (res["status"], out["status"])
+        tr = np.asarray(out["trace"])
+        assert np.all(np.abs(res["trace"][: tr.size] - tr) <= 1e-5 * np.maximum(1.0, np.abs(tr))), (res["trace"], tr)
+        for b, br in enumerate(brs):
+            assert norm_rel(ctx.get_params(b), O.param_vec(br.weights, br.biases)) < 1e-5, b
+        _check_final_targets(ctx, brs, Xs, y, 0.1)
+        for s, br in zip(specs, brs):
+            s["branch"] = f32_branch(br)
+    ctx.close()
