@@ -60,8 +60,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 // global_load "saddr" form: one address VGPR, no 64-bit address arithmetic per piece)
 __device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
+#if BANN_GLDS_NT
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt" ::"s"(m0), "v"(voff), "s"(sbase)
                : "memory", "m0");
+#else
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(m0), "v"(voff), "s"(sbase)
+               : "memory", "m0");
+#endif
 }
 __device__ __forceinline__ void glds4(const void* gsrc, const void* lds_dst) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_off(lds_dst));
