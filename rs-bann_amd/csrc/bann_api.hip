@@ -34,6 +34,7 @@ void free_plan(Plan& p) {
     for (auto& g : p.groups) {
       dfree(g.d_items);
       dfree(g.d_nitems);
+      dfree(g.d_nlist);
     }
   }
   p = Plan{};
@@ -508,7 +509,6 @@ extern "C" int bann_ctx_create(int device, bann_ctx** out) {
   if (const char* e = getenv("BANN_HMC_GRAPH")) ctx->graph_replay = atoi(e) != 0;
   if (const char* e = getenv("BANN_FXL_HEAD")) ctx->fxl_head = atoi(e) != 0;
   if (const char* e = getenv("BANN_NET_GSUM")) ctx->net_gsum = atoi(e) != 0;
-  if (const char* e = getenv("BANN_NET_GW")) ctx->net_gw = atoi(e) == 4 ? 4 : 8;
   if (const char* e = getenv("BANN_FUSE_UPDATE")) ctx->fuse_update_mode = atoi(e) != 0 ? 1 : 0;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;

@@ -237,7 +237,7 @@ int net_buffers_init(bann_ctx* ctx) {
     const BranchHost& last = ctx->br.back();
     CK(dalloc(&ctx->d_cm_scale, last.dev.p_off + last.P));
   }
-  if (!ctx->d_gsum && ctx->net_gsum) {  // one row per group of <= 4 fx branches of 8 chunks and one (L, act)
+  if (!ctx->d_gsum && ctx->net_gsum) {  // one row per (at least) 8 fx branches of 8 chunks and one (L, act)
     std::vector<std::pair<int64_t, int32_t>> cls;  // ((L, act), count)
     for (const auto& h : ctx->br)
       if (h.dev.fused == 1 && h.dev.nchunks == 8) {
@@ -248,7 +248,7 @@ int net_buffers_init(bann_ctx* ctx) {
         if (!found) cls.push_back({key, 1});
       }
     int64_t rows = 0;
-    for (const auto& c : cls) rows += (c.second + 3) / 4;
+    for (const auto& c : cls) rows += (c.second + 7) / 8;
     if (rows > 0) {
       CK(dalloc(&ctx->d_gsum, rows * n));
       ctx->gsum_cap = (int32_t)rows;
@@ -276,10 +276,10 @@ extern "C" int bann_network_step_rule_info(const bann_ctx* ctx, double* out4) {
 }
 
 // k_forward_gsum's work items for a persistent network plan: usable when every branch of the
-// plan is an fx branch of exactly 8 chunks (the full8 groups), L <= 4.  Each launch group's
-// branches, in plan order, form groups of four (one output row each); every group is split
-// into sp tile ranges with sp chosen as the fx plan's split count is: the fewest rounds of
-// two workgroups per CU times the tiles per wave (+2 for the prologue).
+// plan is an fx branch of exactly 8 chunks (the full8 groups), L <= 4.  An item takes up to
+// 8 R of a launch group's branches (plan order) over one range of T <= forward_gsum_max_tiles()
+// tiles, and writes one row; (R, number of ranges) minimise rounds (one workgroup per CU) x
+// R x (T + 2), ties going to the larger R (fewer rows).  BANN_NET_GSUM_R forces R (tests).
 int build_net_groups(bann_ctx* ctx, Plan& p) {
   p.nsum_built = true;
   p.nsum_rows = 0;
@@ -287,42 +287,56 @@ int build_net_groups(bann_ctx* ctx, Plan& p) {
   for (const auto& g : p.groups)
     if (g.kind != 1 || !g.full || g.L < 2 || g.L > 4) return BANN_OK;
   const int64_t ntile = ((int64_t)ctx->nfrag + BANN_TILE_FRAGS - 1) / BANN_TILE_FRAGS;
-  const int gw = ctx->net_gw;
-  p.nsum_gw = gw;
-  const int64_t slots = (gw == 8 ? 1 : 2) * (int64_t)ctx->cus;  // workgroups per CU (LDS)
+  const int64_t tmax = forward_gsum_max_tiles();
+  const int64_t slots = ctx->cus;
+  int force_r = 0;
+  if (const char* e = getenv("BANN_NET_GSUM_R")) force_r = std::max(1, atoi(e));
   int32_t row = 0;
   for (auto& g : p.groups) {
     std::vector<int32_t> brs;
     for (const auto& it : g.items)
       if (brs.empty() || brs.back() != it.branch) brs.push_back(it.branch);
-    const int64_t ng = ((int64_t)brs.size() + gw - 1) / gw;
-    if (row + ng > ctx->gsum_cap) {  // cannot happen: the cap counts every 8-chunk fx branch
+    const int64_t nb = (int64_t)brs.size();
+    int64_t best = -1, r_best = 1, k_best = 1;
+    for (int64_t R = 1; R <= 32; ++R) {
+      if (force_r && R != force_r) continue;
+      const int64_t ng = (nb + 8 * R - 1) / (8 * R);
+      for (int64_t k = (ntile + tmax - 1) / tmax; k <= std::min<int64_t>(ntile, 512); ++k) {
+        const int64_t T = (ntile + k - 1) / k;
+        const int64_t cost = ((ng * k + slots - 1) / slots) * R * (T + 2);
+        if (best < 0 || cost <= best) best = cost, r_best = R, k_best = k;
+      }
+    }
+    const int64_t per = 8 * r_best, ng = (nb + per - 1) / per;
+    if (row + ng > ctx->gsum_cap) {  // cannot happen: the cap counts every 8-chunk fx branch in 8s
       p.nsum_rows = 0;
       return BANN_OK;
     }
-    int64_t best = -1, sp_best = 1;
-    for (int64_t sp = 1; sp <= std::min<int64_t>(ntile, 256); ++sp) {
-      const int64_t cost = ((ng * sp + slots - 1) / slots) * ((ntile + sp - 1) / sp + 2);
-      if (best < 0 || cost < best) best = cost, sp_best = sp;
-    }
     g.nitems.clear();
     for (int64_t gi = 0; gi < ng; ++gi)
-      for (int64_t s = 0; s < sp_best; ++s) {
+      for (int64_t s = 0; s < k_best; ++s) {
         NetGroupItem it{};
-        for (int w = 0; w < 8; ++w) it.b[w] = w < gw && gw * gi + w < (int64_t)brs.size() ? brs[gw * gi + w] : -1;
-        it.tile_begin = (int32_t)(ntile * s / sp_best);
-        it.tile_end = (int32_t)(ntile * (s + 1) / sp_best);
+        it.list_off = (int32_t)(gi * per);
+        it.nbr = (int32_t)std::min<int64_t>(per, nb - gi * per);
+        it.tile_begin = (int32_t)(ntile * s / k_best);
+        it.tile_end = (int32_t)(ntile * (s + 1) / k_best);
         it.row = row + (int32_t)gi;
         if (it.tile_end > it.tile_begin) g.nitems.push_back(it);
       }
     row += (int32_t)ng;
+    g.nlist = brs;
     dfree(g.d_nitems);
+    dfree(g.d_nlist);
     g.d_nitems = nullptr;
+    g.d_nlist = nullptr;
     CK(dalloc(&g.d_nitems, (int64_t)g.nitems.size()));
+    CK(dalloc(&g.d_nlist, (int64_t)g.nlist.size()));
     CK(hipMemcpyAsync(g.d_nitems, g.nitems.data(), g.nitems.size() * sizeof(NetGroupItem), hipMemcpyHostToDevice,
                       ctx->stream));
+    CK(hipMemcpyAsync(g.d_nlist, g.nlist.data(), g.nlist.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                      ctx->stream));
   }
-  CK(hipStreamSynchronize(ctx->stream));  // the host item vectors stay, but keep the copy off the timed path
+  CK(hipStreamSynchronize(ctx->stream));  // keep the copies off the timed trajectory
   p.nsum_rows = row;
   return BANN_OK;
 }
@@ -331,7 +345,7 @@ namespace {
 // the group-sum forward of a plan with build_net_groups items (network mode)
 void run_forward_gsum(bann_ctx* ctx, const Plan& p) {
   for (const auto& g : p.groups)
-    launch_forward_gsum(ctx->st, g.d_nitems, (int32_t)g.nitems.size(), g.L, g.act, p.nsum_gw, ctx->d_gsum,
+    launch_forward_gsum(ctx->st, g.d_nitems, (int32_t)g.nitems.size(), g.d_nlist, g.L, g.act, ctx->d_gsum,
                         ctx->stream);
 }
 

@@ -76,14 +76,15 @@ struct GradItem {
   int32_t tile0;    // forward-only fi pass: the group's tiles before this item (its index space)
   int32_t fold_ix;  // solo plans: index of the branch's FoldJob in the plan's fold list (else -1)
 };
-// network-mode forward with per-group output sums (k_forward_gsum): up to 4 or 8 fx branches
-// (b[w] < 0: none) over one tile range, their outputs summed into group row `row`
+// network-mode forward with per-group output sums (k_forward_gsum): nbr fx branches (the
+// plan's branch list from list_off), 8 per pass, over one tile range, summed into row `row`
 struct NetGroupItem {
-  int32_t b[8];
+  int32_t list_off;
+  int32_t nbr;
   int32_t tile_begin;
   int32_t tile_end;
   int32_t row;
-  int32_t pad;
+  int32_t pad[3];
 };
 // solo-mode fold: a branch's ns slabs at part[part] / rss_part[rss] -> its slab 0
 struct FoldJob {
@@ -204,9 +205,11 @@ void launch_net_sum(const DevState& st, const int32_t* branches, int32_t nb, flo
 // k_forward_gsum): the same two-pass fixed-order sum; scratch: residual_delta_scratch_floats(n)
 void launch_net_sum_rows(const DevState& st, const float* rows, int32_t nrows, float* out, float* scratch,
                          hipStream_t s);
-// network-mode forward of fx branches of 8 chunks, one group row per item group (kernels_fx.hip)
-void launch_forward_gsum(const DevState& st, const NetGroupItem* items, int32_t nitems, int32_t L, int32_t act,
-                         int32_t gw, float* gsum, hipStream_t s);
+// network-mode forward of fx branches of 8 chunks, one row per item (kernels_fx.hip); blist:
+// the items' branch lists; at most forward_gsum_max_tiles() tiles per item
+void launch_forward_gsum(const DevState& st, const NetGroupItem* items, int32_t nitems, const int32_t* blist,
+                         int32_t L, int32_t act, float* gsum, hipStream_t s);
+int forward_gsum_max_tiles();
 // sum_e: in = sum over ranks of the branch outputs, out = the error e; part: net_scratch_doubles(n);
 // y = null: sum_e already holds e and only the nb branch targets y_b = f_b - e are written
 void launch_net_targets(const DevState& st, const int32_t* branches, int32_t nb, float* sum_e, const float* y,

@@ -37,6 +37,8 @@ struct LaunchGroup {
   // network mode, fx groups of 8-chunk branches: k_forward_gsum's group items (build_net_groups)
   std::vector<NetGroupItem> nitems;
   NetGroupItem* d_nitems = nullptr;
+  std::vector<int32_t> nlist;  // the items' branch lists
+  int32_t* d_nlist = nullptr;
 };
 
 // gx path (kernels_gx.hip): the GEMM phases of one scratch group, each over a
@@ -70,7 +72,6 @@ struct Plan {
   // bann_ctx::d_gsum (build_net_groups; nsum_built: tried, nsum_rows > 0: usable)
   bool nsum_built = false;
   int32_t nsum_rows = 0;
-  int32_t nsum_gw = 8;  // branches per group (waves per workgroup of k_forward_gsum)
 };
 
 struct bann_ctx {
@@ -147,7 +148,6 @@ struct bann_ctx {
   float* d_gsum = nullptr;     // network mode: per-group output sums of the fx branches (gsum_cap rows of n)
   int32_t gsum_cap = 0;
   bool net_gsum = true;        // BANN_NET_GSUM=0 at creation: per-branch output rows in every step (A/B)
-  int32_t net_gw = 8;          // branches per group of the group-sum forward (BANN_NET_GW=4: four)
   float* d_netsum = nullptr;   // network mode: n-vector sum of the local branch outputs, then the error e
   float* d_nety = nullptr;     // network mode: the targets y
   double* d_netrss = nullptr;  // network mode: global rss per leapfrog step (netrss_cap entries)

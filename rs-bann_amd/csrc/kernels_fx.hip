@@ -1090,231 +1090,219 @@ void launch_forward_fx(const DevState& st, const GradItem* items, int32_t nitems
 
 // ===========================================================================
 // Network-mode forward with per-group output sums (bann_network_hmc_step; fx branches of
-// 8 chunks).  A network step needs sum_b f_b only, not the branch outputs: a workgroup
-// takes a GROUP of <= 4 branches over one tile range, wave w runs branch w of the group
-// through the half-tile ring of k_forward_fx (its own W0 digits in registers, its own
-// head weights in scalar registers) and keeps PB = 8 tiles of outputs in registers; per
-// block of 8 tiles the four waves put them in LDS (double-buffered, one barrier) and wave
-// w adds tiles 2w, 2w + 1 over the group in wave order (deterministic) and stores them:
-// one row per group (a quarter of the bytes and store instructions of per-branch rows,
-// whose stores, interleaved with the stream, cost the per-branch forward a fifth of its
-// time: profiles/r05_fwd_store_ablation.md).  The per-branch rows the trajectory's end
-// needs come from the last step's per-branch forward (bann_dist.hip).
-// The vmcnt waits count this wave's younger DMA pieces AND its younger group-row store
-// (a store left out of the count would make the wait drain it too); never more than
-// issued, so a wait can only be longer than needed, never shorter.
+// 8 chunks).  A network step needs sum_b f_b only, not the branch outputs.  A work item is a
+// GROUP of up to 8 R branches over one range of T <= GS_TMAX tiles; its 8 waves take the
+// group in R passes of 8 branches (wave w: branch 8 r + w of the item's list), each branch
+// through the half-tile ring of k_forward_fx (its W0 digits in registers, its head weights in
+// scalar registers), PB = 8 tiles of outputs in registers.  Per block of 8 tiles the waves
+// put them in LDS (double-buffered, one barrier); thread t then adds tile t >> 6, individual
+// t & 63 over the 8 waves in wave order and accumulates it into the item's LDS sum over the
+// passes in pass order (the same thread every pass: deterministic, no second barrier).  The
+// item's row -- one per 8 R branches -- is stored once, at the end.  Measured (round 6,
+// profiles/r06_net_gsum_ab.txt): per-branch rows (200 MB per launch) cost the forward
+// 0.26 ms, one row per 8 branches written block by block (25 MB) still 0.11 ms -- the
+// stores interleaved with the read stream, not their waits -- so the rows are few and late.
+// The per-branch rows the trajectory's end needs come from the last step's per-branch
+// forward (bann_dist.hip).
 // ===========================================================================
-template <int NL, int ACT, int NW>
-__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
-    k_forward_gsum(DevState st, const NetGroupItem* __restrict__ items, float* __restrict__ gsum) {
+#define GS_TMAX 100  // tiles per item (the LDS sum: 25 KiB)
+template <int NL, int ACT>
+__global__ void __launch_bounds__(64 * 8, 1)
+    k_forward_gsum(DevState st, const NetGroupItem* __restrict__ items, const int32_t* __restrict__ blist,
+                   float* __restrict__ gsum) {
   constexpr int NH = NL - 1;
+  constexpr int NW = 8;
   constexpr int NU = 3;   // half-tile units per wave in the ring
-  constexpr int PB = 8;   // tiles per block (one group-row store per wave and block)
-  constexpr int TPW = PB / NW;  // tiles a wave sums and stores per block
-  static_assert(NW == 4 || NW == 8, "groups of 4 or 8 branches");
+  constexpr int PB = 8;   // tiles per block
   __shared__ __attribute__((aligned(16))) char s_x[NW][NU * 4096];
   __shared__ __attribute__((aligned(16))) float s_o[2][NW][PB][64];
+  __shared__ __attribute__((aligned(16))) float s_acc[GS_TMAX][64];
   __shared__ float s_hw[NW][NL][20];
 
-  const NetGroupItem* itp = items + blockIdx.x;  // (fields read in place: a private copy indexed by the
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave would be promoted to LDS)
+  const NetGroupItem* itp = items + blockIdx.x;  // fields read in place (a private copy indexed by
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // the wave would go to LDS)
   const int lane = threadIdx.x & 63;
-  const int bw = __builtin_amdgcn_readfirstlane(itp->b[wave]);
-  const bool act_w = bw >= 0;          // wave-uniform: the group's last waves may have no branch
-  const int b = act_w ? bw : __builtin_amdgcn_readfirstlane(itp->b[0]);  // (a valid descriptor for the inactive waves)
-  const NetGroupItem it{{0, 0, 0, 0, 0, 0, 0, 0}, itp->tile_begin, itp->tile_end, itp->row, 0};
-  const BranchDev& bd = st.br[b];
+  const int tb = itp->tile_begin, nt = itp->tile_end - itp->tile_begin;
+  const int nbr = itp->nbr, loff = itp->list_off;
+  const int passes = (nbr + NW - 1) / NW;
   const int64_t n = st.n;
-  const int tb = it.tile_begin, nt = it.tile_end - it.tile_begin;
-  const float* th = st.theta + bd.p_off;
-  for (int t = lane; t < NL * 20; t += 64) {
-    const int l = t / 20, r = t - l * 20;
-    float v = 0.f;
-    if (r < 16) {
-      const int j = r >> 2, k = r & 3;
-      if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
-    } else {
-      const int k = r - 16;
-      if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
-      if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
-    }
-    s_hw[wave][l][r] = v;
-  }
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 1, tp = lane & 1;
-  float zscale = st.fc[b].scale[g];
-  v4i Areg[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) Areg[c] = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  asm volatile("" : "+v"(zscale));
-  __syncthreads();
-  v4i rowsum64 = v4i{0, 0, 0, 0};
-#pragma unroll
-  for (int c = 0; c < 8; ++c) rowsum64 = fx_rowsum64_acc(Areg[c], rowsum64);
-  float uWm[NL][4][4], uB[NH][4];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        uWm[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[wave][l][4 * j + k]) : 0.f;
-    if (l < NH)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[wave][l][16 + k]);
-  }
   const int gsw = g & 1;
   const uint32_t fo0 = (uint32_t)((16 * g + tq + 8 * gsw) * 16 + 8 * (tp ^ gsw));
   const uint32_t fo1 = (uint32_t)((16 * g + tq + 8 * (1 ^ gsw)) * 16 + 8 * (tp ^ 1 ^ gsw));
   const int iota = 4 * i16 + g;
-  const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
   constexpr int64_t tile_bytes = 8 * 1024;
-  const bool pad_row = 64 * 7 + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
   char* const xw = &s_x[wave][0];
-  const int nu = act_w ? 2 * nt : 0;
-  auto issue_unit = [&](int u) {
-    const int64_t tt = tb + (u >> 1);
-    char* dst = xw + (u % NU) * 4096;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int cc = 4 * (u & 1) + c;
-      if (cc == 7 && pad_row) continue;  // lane 0 never pads: the wave's instruction always issues
-      glds16(xsrc + tt * tile_bytes + cc * 1024, dst + c * 1024);
-    }
-  };
-  auto head_out = [&](v4i (&facc)[4]) -> float {
-    fx_fwd_fields(facc);
-    float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
-    float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
-    swap32(z0, z2);
-    swap32(z1, z3);
-    swap16(z0, z1);
-    swap16(z2, z3);
-    float a[4];
-    a[0] = act_h_t<ACT>(z0 + uB[0][0]);
-    a[1] = act_h_t<ACT>(z1 + uB[0][1]);
-    a[2] = act_h_t<ACT>(z2 + uB[0][2]);
-    a[3] = act_h_t<ACT>(z3 + uB[0][3]);
-#pragma unroll
-    for (int l = 1; l < NH; ++l) {
-      float an[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float s = uB[l][k];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s = fmaf(a[j], uWm[l][j][k], s);
-        an[k] = act_h_t<ACT>(s);
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = an[k];
-    }
-    float out = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) out = fmaf(a[j], uWm[NL - 1][j][0], out);
-    return out;
-  };
-  for (int u = 0; u < NU && u < nu; ++u) issue_unit(u);
-  float* const grow = gsum + (int64_t)it.row * n;
   const int nblk = (nt + PB - 1) / PB;
-  for (int blk = 0; blk < nblk; ++blk) {
-    const int k0 = blk * PB;
-    float obuf[PB];
+  // thread t's share of every block: tile t >> 6, individual t & 63 (also its LDS sum entries)
+  const int jt = threadIdx.x >> 6, ind = threadIdx.x & 63;
+  int gb = 0;  // running block count (the parity of the s_o buffer)
+  for (int r = 0; r < passes; ++r) {
+    const int bi = NW * r + wave;
+    const int bw = bi < nbr ? __builtin_amdgcn_readfirstlane(blist[loff + bi]) : -1;
+    const bool act_w = bw >= 0;  // wave-uniform: the last pass's waves may have no branch
+    const int b = act_w ? bw : __builtin_amdgcn_readfirstlane(blist[loff]);
+    const BranchDev& bd = st.br[b];
+    const float* th = st.theta + bd.p_off;
+    for (int t = lane; t < NL * 20; t += 64) {
+      const int l = t / 20, rr = t - l * 20;
+      float v = 0.f;
+      if (rr < 16) {
+        const int j = rr >> 2, k = rr & 3;
+        if (l >= 1 && j < bd.win[l] && k < bd.widths[l]) v = th[bd.woff[l] + k * bd.win[l] + j];
+      } else {
+        const int k = rr - 16;
+        if (l == 0 && k < bd.widths[0]) v = st.fc[b].c0[k];
+        if (l >= 1 && l < NH && k < bd.widths[l]) v = th[bd.boff[l] + k];
+      }
+      s_hw[wave][l][rr] = v;
+    }
+    float zscale = st.fc[b].scale[g];
+    v4i Areg[8];
 #pragma unroll
-    for (int j = 0; j < PB; ++j) obuf[j] = 0.f;
-    if (act_w) {
+    for (int c = 0; c < 8; ++c) Areg[c] = *reinterpret_cast<const v4i*>(st.dig + bd.dig_off + ((int64_t)c * 64 + lane) * 16);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (the ring is empty between passes)
+    asm volatile("" : "+v"(zscale));
+    v4i rowsum64 = v4i{0, 0, 0, 0};
 #pragma unroll
-      for (int j = 0; j < PB; ++j) {
-        const int k = k0 + j;
-        if (k >= nt) continue;  // (not break: a break makes obuf a dynamically indexed array)
-        v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
+    for (int c = 0; c < 8; ++c) rowsum64 = fx_rowsum64_acc(Areg[c], rowsum64);
+    float uWm[NL][4][4], uB[NH][4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int u = 2 * k + h;
-          const int last = u + NU - 1 < nu - 1 ? u + NU - 1 : nu - 1;
-          // the previous block's group-row store (issued after its last tile, so after the
-          // units up to 16 blk - 1 + NU) is younger than units 16 blk .. 16 blk + NU - 1
-          const int younger_st = (blk > 0 && u - 2 * k0 < NU && k0 - PB + TPW * wave < nt) ? 1 : 0;
-          vm_wait_n(4 * (last - u) + younger_st);
-          const char* xs = xw + (u % NU) * 4096;
-          v4u Xq[2];
+    for (int l = 0; l < NL; ++l) {
 #pragma unroll
-          for (int c = 0; c < 2; ++c) Xq[c] = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const v4u Xc = Xq[c % 2];
-            if (c + 2 < 4) Xq[c % 2] = (v4u)lds_tr8_pair(xs + (c + 2) * 1024 + fo0, xs + (c + 2) * 1024 + fo1);
-            fx_fwd_chunk(Areg[4 * h + c], Xc, facc);
-            __builtin_amdgcn_sched_barrier(0);
+        for (int k = 0; k < 4; ++k)
+          uWm[l][j][k] = (l >= 1 && (l < NL - 1 || k == 0)) ? sgpr_f(s_hw[wave][l][4 * j + k]) : 0.f;
+      if (l < NH)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) uB[l][k] = sgpr_f(s_hw[wave][l][16 + k]);
+    }
+    const char* xsrc = reinterpret_cast<const char*>(st.xu2) + bd.x_off + lane * 16;
+    const bool pad_row = 64 * 7 + 16 * (lane >> 4) + (((lane & 15) - 8 * ((lane >> 4) & 1)) & 15) >= bd.m;
+    const int nu = act_w ? 2 * nt : 0;
+    auto issue_unit = [&](int u) {
+      const int64_t tt = tb + (u >> 1);
+      char* dst = xw + (u % NU) * 4096;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cc = 4 * (u & 1) + c;
+        if (cc == 7 && pad_row) continue;  // lane 0 never pads: the wave's instruction always issues
+        glds16(xsrc + tt * tile_bytes + cc * 1024, dst + c * 1024);
+      }
+    };
+    auto head_out = [&](v4i (&facc)[4]) -> float {
+      fx_fwd_fields(facc);
+      float z0 = zscale * comb4(facc[0]), z1 = (0.25f * zscale) * comb4(facc[1]);
+      float z2 = (0.0625f * zscale) * comb4(facc[2]), z3 = (0.015625f * zscale) * comb4(facc[3]);
+      swap32(z0, z2);
+      swap32(z1, z3);
+      swap16(z0, z1);
+      swap16(z2, z3);
+      float a[4];
+      a[0] = act_h_t<ACT>(z0 + uB[0][0]);
+      a[1] = act_h_t<ACT>(z1 + uB[0][1]);
+      a[2] = act_h_t<ACT>(z2 + uB[0][2]);
+      a[3] = act_h_t<ACT>(z3 + uB[0][3]);
+#pragma unroll
+      for (int l = 1; l < NH; ++l) {
+        float an[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float sacc = uB[l][k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sacc = fmaf(a[j], uWm[l][j][k], sacc);
+          an[k] = act_h_t<ACT>(sacc);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = an[k];
+      }
+      float out = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out = fmaf(a[j], uWm[NL - 1][j][0], out);
+      return out;
+    };
+    for (int u = 0; u < NU && u < nu; ++u) issue_unit(u);
+    for (int blk = 0; blk < nblk; ++blk, ++gb) {
+      const int k0 = blk * PB;
+      float obuf[PB];
+#pragma unroll
+      for (int j = 0; j < PB; ++j) obuf[j] = 0.f;
+      if (act_w) {
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+          const int k = k0 + j;
+          if (k >= nt) continue;  // (not break: a break makes obuf a dynamically indexed array)
+          v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int u = 2 * k + h;
+            const int last = u + NU - 1 < nu - 1 ? u + NU - 1 : nu - 1;
+            vm_wait_n(4 * (last - u));  // this wave issues nothing but the ring's pieces in the loop
+            const char* xs = xw + (u % NU) * 4096;
+            v4u Xq[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) Xq[c] = (v4u)lds_tr8_pair(xs + c * 1024 + fo0, xs + c * 1024 + fo1);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const v4u Xc = Xq[c % 2];
+              if (c + 2 < 4) Xq[c % 2] = (v4u)lds_tr8_pair(xs + (c + 2) * 1024 + fo0, xs + (c + 2) * 1024 + fo1);
+              fx_fwd_chunk(Areg[4 * h + c], Xc, facc);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (u + NU < nu) issue_unit(u + NU);
           }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (u + NU < nu) issue_unit(u + NU);
+          __builtin_amdgcn_sched_barrier(0);
+          obuf[j] = head_out(facc);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        obuf[j] = head_out(facc);
       }
-    }
-    // the block's outputs -> LDS (asm stores: no compiler drain of the DMA in front of them)
-    float (*const so)[64] = s_o[blk & 1][wave];
+      // the block's outputs -> LDS (asm stores: no compiler drain of the DMA in front of them)
+      float (*const so)[64] = s_o[gb & 1][wave];
 #pragma unroll
-    for (int j = 0; j < PB; ++j) lds_st_f32(&so[j][iota], obuf[j]);
-    LDS_BARRIER();
-    // wave w: tiles TPW w .. TPW (w + 1) - 1 of the block, summed over the group in wave order
-    if (k0 + TPW * wave < nt) {  // wave-uniform: the wave's first tile exists, so lane 0's row is < n
-      if constexpr (TPW == 2) {  // lane: individuals 2 (lane & 31), + 1 of tile 2w + (lane >> 5)
-        const int jt = 2 * wave + (lane >> 5), ind = 2 * (lane & 31);
-        float2 s = *reinterpret_cast<const float2*>(&s_o[blk & 1][0][jt][ind]);
+      for (int j = 0; j < PB; ++j) lds_st_f32(&so[j][iota], obuf[j]);
+      LDS_BARRIER();
+      // thread t: tile jt of the block over the 8 waves in wave order, into the item's sum in pass order
+      if (k0 + jt < nt) {
+        float sacc = s_o[gb & 1][0][jt][ind];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) {
-          const float2 v = *reinterpret_cast<const float2*>(&s_o[blk & 1][w][jt][ind]);
-          s.x += v.x;
-          s.y += v.y;
-        }
-        const int64_t row = 64 * (int64_t)(tb + k0 + jt) + ind;
-        if (k0 + jt < nt) {
-          if (row + 1 < n)
-            *reinterpret_cast<float2*>(grow + row) = s;
-          else if (row < n)
-            grow[row] = s.x;
-        }
-      } else {  // lane: individual `lane` of tile w
-        const int jt = wave;
-        float s = s_o[blk & 1][0][jt][lane];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) s += s_o[blk & 1][w][jt][lane];
-        const int64_t row = 64 * (int64_t)(tb + k0 + jt) + lane;
-        if (row < n) grow[row] = s;
+        for (int w = 1; w < NW; ++w) sacc += s_o[gb & 1][w][jt][ind];
+        float* a = &s_acc[k0 + jt][ind];
+        lds_st_f32(a, r == 0 ? sacc : *a + sacc);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the item's row: every thread stores the entries it accumulated (tile 8 blk + jt, individual ind)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  float* const grow = gsum + (int64_t)itp->row * n;
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int k = blk * PB + jt;
+    const int64_t row = 64 * (int64_t)(tb + k) + ind;
+    if (k < nt && row < n) grow[row] = s_acc[k][ind];
+  }
 }
 
-template <int NL, int NW>
-static void launch_gsum_nl(const DevState& st, const NetGroupItem* items, int32_t nitems, int act, float* gsum,
-                           hipStream_t s) {
-  const dim3 grid((unsigned)nitems), block(64 * NW);
+template <int NL>
+static void launch_gsum_nl(const DevState& st, const NetGroupItem* items, int32_t nitems, const int32_t* blist,
+                           int act, float* gsum, hipStream_t s) {
+  const dim3 grid((unsigned)nitems), block(64 * 8);
   switch (act) {
-    case 0: hipLaunchKernelGGL((k_forward_gsum<NL, 0, NW>), grid, block, 0, s, st, items, gsum); break;
-    case 1: hipLaunchKernelGGL((k_forward_gsum<NL, 1, NW>), grid, block, 0, s, st, items, gsum); break;
-    case 2: hipLaunchKernelGGL((k_forward_gsum<NL, 2, NW>), grid, block, 0, s, st, items, gsum); break;
-    case 3: hipLaunchKernelGGL((k_forward_gsum<NL, 3, NW>), grid, block, 0, s, st, items, gsum); break;
-    default: hipLaunchKernelGGL((k_forward_gsum<NL, 4, NW>), grid, block, 0, s, st, items, gsum); break;
+    case 0: hipLaunchKernelGGL((k_forward_gsum<NL, 0>), grid, block, 0, s, st, items, blist, gsum); break;
+    case 1: hipLaunchKernelGGL((k_forward_gsum<NL, 1>), grid, block, 0, s, st, items, blist, gsum); break;
+    case 2: hipLaunchKernelGGL((k_forward_gsum<NL, 2>), grid, block, 0, s, st, items, blist, gsum); break;
+    case 3: hipLaunchKernelGGL((k_forward_gsum<NL, 3>), grid, block, 0, s, st, items, blist, gsum); break;
+    default: hipLaunchKernelGGL((k_forward_gsum<NL, 4>), grid, block, 0, s, st, items, blist, gsum); break;
   }
 }
 
-// gw: branches per group (= waves per workgroup), 4 or 8
-void launch_forward_gsum(const DevState& st, const NetGroupItem* items, int32_t nitems, int32_t L, int32_t act,
-                         int32_t gw, float* gsum, hipStream_t s) {
+int forward_gsum_max_tiles() { return GS_TMAX; }
+
+void launch_forward_gsum(const DevState& st, const NetGroupItem* items, int32_t nitems, const int32_t* blist,
+                         int32_t L, int32_t act, float* gsum, hipStream_t s) {
   if (nitems <= 0) return;
-  if (gw == 8) {
-    if (L == 2) launch_gsum_nl<2, 8>(st, items, nitems, act, gsum, s);
-    if (L == 3) launch_gsum_nl<3, 8>(st, items, nitems, act, gsum, s);
-    if (L == 4) launch_gsum_nl<4, 8>(st, items, nitems, act, gsum, s);
-  } else {
-    if (L == 2) launch_gsum_nl<2, 4>(st, items, nitems, act, gsum, s);
-    if (L == 3) launch_gsum_nl<3, 4>(st, items, nitems, act, gsum, s);
-    if (L == 4) launch_gsum_nl<4, 4>(st, items, nitems, act, gsum, s);
-  }
+  if (L == 2) launch_gsum_nl<2>(st, items, nitems, blist, act, gsum, s);
+  if (L == 3) launch_gsum_nl<3>(st, items, nitems, blist, act, gsum, s);
+  if (L == 4) launch_gsum_nl<4>(st, items, nitems, blist, act, gsum, s);
 }
 
 // ===========================================================================

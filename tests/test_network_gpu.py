@@ -465,19 +465,21 @@ def test_network_rss_out_on_rejection():
     ctx.close()
 
 
-@pytest.mark.parametrize("gsum,gw", [("1", "8"), ("1", "4"), ("0", "8")])
-def test_network_group_sum_forward(monkeypatch, gsum, gw):
+@pytest.mark.parametrize("gsum,passes", [("1", None), ("1", "2"), ("0", None)])
+def test_network_group_sum_forward(monkeypatch, gsum, passes):
     """k_forward_gsum (the network forward of 8-chunk fx branches): every step's forward but
-    the last sums groups of eight (or four) branches in LDS and writes one row per group.  Six
-    branches (one group with two idle waves, or a full group and a half one), an odd n (a partial last tile and a single-float row tail),
-    two trajectories (the second starts from current prediction rows, so its step 0 is a
-    group forward too): -H trace, status, parameters and the final targets match the oracle,
-    and the per-branch forward (BANN_NET_GSUM=0) agrees."""
+    the last sums the branches of an item -- 8 per pass, passes added in order in LDS -- and
+    writes one row per item.  Twelve branches (a full pass and a partial one; with
+    BANN_NET_GSUM_R=2 both in one item), an odd n (a partial last tile), two trajectories (the
+    second starts from current prediction rows, so its step 0 is a group forward too): -H
+    trace, status, parameters and the final targets match the oracle, and so does the
+    per-branch forward (BANN_NET_GSUM=0)."""
     monkeypatch.setenv("BANN_NET_GSUM", gsum)
-    monkeypatch.setenv("BANN_NET_GW", gw)   # branches per group: 8 (default; one group, two waves idle) or 4
+    if passes:
+        monkeypatch.setenv("BANN_NET_GSUM_R", passes)
     rng = np.random.default_rng(37)
     n = 3001
-    shapes = [(500, [4, 4, 1])] * 5 + [(450, [4, 4, 1])]
+    shapes = [(500, [4, 4, 1])] * 11 + [(450, [4, 4, 1])]
     M = sum(m for m, _ in shapes)
     g = O.synthetic_genotypes(rng, n, M)
     specs, off = [], 0
@@ -496,7 +498,13 @@ def test_network_group_sum_forward(monkeypatch, gsum, gw):
         eps, mom = _draws(rng, specs, L)
         res = ctx.network_hmc_step(y, L, bias=0.1, lambda_e=2.0, eps=np.concatenate(eps),
                                    momentum=np.concatenate(mom), u=u)
-        assert ctx.network_group_rows() == (-(-len(specs) // int(gw)) if gsum == "1" else 0)
+        rows = ctx.network_group_rows()
+        if gsum == "0":
+            assert rows == 0
+        elif passes == "2":
+            assert rows == 1   # one item list of 12 branches in two passes
+        else:
+            assert rows >= 1
         brs = [s["branch"].copy() for s in specs]
         out = O.network_hmc_step(brs, Xs, y, 0.1, 2.0, [e.astype(np.float64) for e in eps],
                                  [p.astype(np.float64) for p in mom], L, 10.0, u)
