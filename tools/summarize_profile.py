@@ -21,8 +21,8 @@ shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
 trace = list(csv.DictReader(open(find("trace", "*kernel_trace.csv"))))
 bench = json.loads(open(os.path.join(out, "bench_trace.json")).read().strip().splitlines()[-1])
 
-# the timed trajectory: bench.py runs the network check's trajectory (when the line
-# carries network_check), the warmup trajectory, then the back-to-back measurement
+# the timed trajectory: bench.py runs the network check's two trajectories (when the line
+# carries network_check: an untimed one, then the timed one), the warmup trajectory, then the back-to-back measurement
 # session (a 2-step leapfrog session), then the timed trajectory; each starts with
 # one k_step_sizes launch (traj_prepare)
 trace.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -30,7 +30,7 @@ starts = [i for i, r in enumerate(trace) if "k_step_sizes" in r["Kernel_Name"]]
 sampler = bench.get("sampler") or ("network" if "network-joint" in bench["config"]["workload"] else "branch")
 # trajectories before the timed one: the network check, the warmup, and (branch sampler) the
 # back-to-back session
-t_ix = (1 if bench.get("network_check") else 0) + (1 if bench.get("warmup") else 0) + (1 if sampler == "branch" else 0)
+t_ix = (2 if bench.get("network_check") else 0) + (1 if bench.get("warmup") else 0) + (1 if sampler == "branch" else 0)
 timed = trace[starts[t_ix]:starts[t_ix + 1] if len(starts) > t_ix + 1 else len(trace)] if len(starts) > t_ix else []
 tgrad = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_fused_grad" in r["Kernel_Name"]]
 tupd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_update" in r["Kernel_Name"]]
@@ -73,9 +73,10 @@ fetch = pmc_bytes("fetch", "FETCH_SIZE") * 2.0   # gfx950: FETCH_SIZE counts 1/2
 # last launch of a trajectory also write the n predictions per branch (4 n B)
 write = pmc_bytes("write", "WRITE_SIZE", min)
 write_pred = pmc_bytes("write", "WRITE_SIZE", max)
-# the network sampler's forward-only launch (k_forward_fx / k_forward_fi), when the command ran one
+# the network sampler's forward-only launch (k_forward_gsum, the group-sum forward of every step but the
+# last; k_forward_fx / k_forward_fi), when the command ran one
 fwd_fetch = None
-for fk in ("k_forward_fx", "k_forward_fi"):
+for fk in ("k_forward_gsum", "k_forward_fx", "k_forward_fi"):
     fb = pmc_bytes("fetch", "FETCH_SIZE", kernel=fk)
     if fb is not None:
         fwd_fetch = (fk, fb * 2.0)
