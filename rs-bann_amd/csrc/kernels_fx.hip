@@ -71,27 +71,16 @@
 #ifndef FX_STAMPS
 #define FX_STAMPS 0
 #endif
-// scheduling knobs of the tile loop (tools/build_ab.sh variants; the product values)
-#ifndef FXT_PF
-#define FXT_PF 1  // forward wave priority
-#endif
-#ifndef FXT_PH
-#define FXT_PH 1  // head + delta0 digit priority
-#endif
-#ifndef FXT_PB
-#define FXT_PB 0  // backward priority
-#endif
-#ifndef FXT_FD
-#define FXT_FD 2  // forward: LDS reads this many chunks ahead
-#endif
+// the backward's genotype-window prefetch depth and its per-window scheduling barrier (round 6,
+// kbench and C3 line A/B on one box: PD 8 -> 12 without the barrier, fx 1.181 / 1.190 -> 1.173 /
+// 1.169 ms, 780.7 / 774.5 -> 785.4 / 787.1 steps/s; a barrier-free PD 8: 1.175 / 1.177; measured and
+// not kept: the forward at priority 0, the head at 2, the backward at 1, the forward three chunks
+// ahead, PD 4 or 16, no barrier per forward chunk -- tools/gpu_kab.sh, profiles/r06_fx_knobs.txt)
 #ifndef FXT_PD
-#define FXT_PD 8  // backward: genotype window reads this many windows ahead
-#endif
-#ifndef FXT_SBF
-#define FXT_SBF 1  // a scheduling barrier after each forward chunk
+#define FXT_PD 12  // backward: genotype window reads this many windows ahead
 #endif
 #ifndef FXT_SBB
-#define FXT_SBB 1  // a scheduling barrier after each backward window
+#define FXT_SBB 0  // a scheduling barrier after each backward window (1: the round-5 schedule)
 #endif
 #ifndef FX_ABL
 #define FX_ABL 0
@@ -391,9 +380,9 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     v4i facc[4] = {v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, v4i{0, 0, 0, 0}, rowsum64};
     // the forward at raised priority too (with the stream issued in the backward:
     // -1.2 % per launch, A/B on one box)
-    __builtin_amdgcn_s_setprio(FXT_PF);
+    __builtin_amdgcn_s_setprio(1);
     {
-      constexpr int FD = FXT_FD;  // two chunks ahead: an LDS read's latency exceeds one chunk's 4 MFMAs
+      constexpr int FD = 2;  // two chunks ahead: an LDS read's latency exceeds one chunk's 4 MFMAs
       v4u Xq[FD];
       v4i Aq[FD];
 #pragma unroll
@@ -427,7 +416,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
         facc[1] = FX_MFMA(Ac, B1, facc[1]);
         facc[2] = FX_MFMA(Ac, B2, facc[2]);
         facc[3] = FX_MFMA(Ac, B3, facc[3]);
-        if (FXT_SBF) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -435,7 +424,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
     // the head + digit phase is a dependent VALU chain: at raised priority it
     // takes the SIMD's issue slots ahead of the partner wave's independent
     // MFMA/unpack stream (measured -1 %)
-    __builtin_amdgcn_s_setprio(FXT_PH);
+    __builtin_amdgcn_s_setprio(1);
     // lane (column g, slot i16) holds individual 4 i16 + q in register q; transpose
     // so that lane L holds all four columns of individual 4 (L & 15) + (L >> 4)
     fx_fwd_fields(facc);  // F_q = 4^q S_q, exact
@@ -574,7 +563,7 @@ __global__ void __launch_bounds__(64 * FX_WAVES, NL == 4 ? 1 : 2)
 
     __builtin_amdgcn_sched_barrier(0);
     FX_STAMP(3);
-    __builtin_amdgcn_s_setprio(FXT_PB);
+    __builtin_amdgcn_s_setprio(0);
     // ---- backward: dW0 digit sums += G^T delta0 (reads 4 windows ahead) ----
     const v4i A = lds_tr8_pair(sd_r, sd_r + 8 * 16);
     acc3 = FX_MFMA(A, FX_ONES3, acc3);
