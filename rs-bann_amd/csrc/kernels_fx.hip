@@ -1344,6 +1344,14 @@ void launch_forward_gsum(const DevState& st, const NetGroupItem* items, int32_t 
 #ifndef FXL_PD
 #define FXL_PD 8  // backward genotype-window prefetch depth
 #endif
+// fxh compute waves without the per-window / per-chunk scheduling barriers (round 6, kbench at C2,
+// three alternating reps: 0.0921 -> 0.0888 ms per launch; either alone 0.0899 / ~0.092; profiles/r06_fx_knobs.txt)
+#ifndef FXH_SBB
+#define FXH_SBB 0  // a scheduling barrier after each backward window (1: the round-5 schedule)
+#endif
+#ifndef FXH_SBF
+#define FXH_SBF 0  // a scheduling barrier after each forward chunk (1: the round-5 schedule)
+#endif
 #ifndef FXL_DPRE
 #define FXL_DPRE 31  // backward window after which the next tile's first digit loads issue (earlier: spills)
 #endif
@@ -2231,7 +2239,7 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
             asm volatile("" ::"v"(Bn2));
             if (refill) glds16(rsrc + (u >> 2) * 1024, xslot0 + (k % NSL) * SLOT + (u >> 2) * 1024);
           }
-          __builtin_amdgcn_sched_barrier(0);
+          if (FXH_SBB) __builtin_amdgcn_sched_barrier(0);
         }
       }
       // ---- forward of tile p: partial Z0 over this wave's chunks -> exchange slot p % 2 ----
@@ -2249,7 +2257,7 @@ __global__ void __launch_bounds__(64 * (FXH_MAXC + 1), 1)
           v4u Xn = Xc;
           if (c + 1 < CW) Xn = (v4u)lds_tr8_pair(xs + (c + 1) * 1024 + fo0, xs + (c + 1) * 1024 + fo1);
           fx_fwd_chunk(Dres[c], Xc, facc);
-          __builtin_amdgcn_sched_barrier(0);
+          if (FXH_SBF) __builtin_amdgcn_sched_barrier(0);
           Xc = Xn;
         }
         fx_fwd_fields(facc);
