@@ -518,6 +518,12 @@ def main():
         b2b_grad_ms, b2b_upd_ms = b2b_session(restore=True)
     if args.warmup:
         trajectory(args.warmup, seed=7 + rank)
+    if args.sampler == "network":
+        # the network line has no back-to-back session (it would move the joint state): one more
+        # untimed trajectory of K steps (burn-in) settles the GPU clock under the trajectory's own
+        # load -- without it the timed trajectory's first gradient launches ran 1.3-1.6 ms against
+        # 1.10 later (profiles/r06c_net_summary.md, the power controller's transient)
+        trajectory(args.steps, seed=5 + rank)
     # network sampler, common-mode rule (auto): the warmup trajectory adapted the step factors
     # (burn-in); the timed and the acceptance trajectories apply them frozen -- step sizes
     # independent of each trajectory's start, as HMC's reversibility asks

@@ -30,7 +30,8 @@ starts = [i for i, r in enumerate(trace) if "k_step_sizes" in r["Kernel_Name"]]
 sampler = bench.get("sampler") or ("network" if "network-joint" in bench["config"]["workload"] else "branch")
 # trajectories before the timed one: the network check, the warmup, and (branch sampler) the
 # back-to-back session
-t_ix = (2 if bench.get("network_check") else 0) + (1 if bench.get("warmup") else 0) + (1 if sampler == "branch" else 0)
+t_ix = (2 if bench.get("network_check") else 0) + (1 if bench.get("warmup") else 0) + (1 if sampler == "branch" else 0) \
+    + (1 if sampler == "network" else 0)   # the network line's settling trajectory
 timed = trace[starts[t_ix]:starts[t_ix + 1] if len(starts) > t_ix + 1 else len(trace)] if len(starts) > t_ix else []
 tgrad = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_fused_grad" in r["Kernel_Name"]]
 tupd = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed if "k_update" in r["Kernel_Name"]]
