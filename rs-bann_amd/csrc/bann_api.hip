@@ -544,6 +544,7 @@ extern "C" int bann_ctx_destroy(bann_ctx* ctx) {
   comm_destroy(ctx);
   for (void* p : bufs) dfree(p);
   if (ctx->h_status) (void)hipHostFree(ctx->h_status);
+  if (ctx->h_par_stage) (void)hipHostFree(ctx->h_par_stage);
   if (ctx->h_delta) (void)hipHostFree(ctx->h_delta);
   if (ctx->h_res_stat) (void)hipHostFree(ctx->h_res_stat);
   if (ctx->plan_ev_pending && ctx->ev_plan) (void)hipEventSynchronize(ctx->ev_plan);
@@ -1061,6 +1062,11 @@ extern "C" int bann_finalize(bann_ctx* ctx, int32_t free_raw) {
   CK(dalloc(&ctx->d_delta, n));
   CK(dalloc(&ctx->d_delta_part, residual_delta_scratch_floats(n)));
   CK(hipHostMalloc((void**)&ctx->h_status, nb * sizeof(int32_t), hipHostMallocDefault));
+  {
+    int64_t max_p = 1;
+    for (const auto& h : ctx->br) max_p = std::max<int64_t>(max_p, h.P);
+    CK(hipHostMalloc((void**)&ctx->h_par_stage, max_p * sizeof(float), hipHostMallocDefault));
+  }
   CK(hipHostMalloc((void**)&ctx->h_delta, n * sizeof(float), hipHostMallocDefault));
   CK(hipMemsetAsync(ctx->d_pred0, 0, nb * n * sizeof(float), ctx->stream));
   CK(dalloc(&ctx->d_scr, scr_off));
@@ -1854,6 +1860,55 @@ extern "C" int bann_hmc_step(bann_ctx* ctx, const int32_t* branches, int32_t nb,
     if (rc2) return rc2;
   }
   return hmc_outputs(ctx, branches, nb, L, status_out, h_trace_out, uturn_out, log_density_out);
+}
+
+// The sequential driver's branch-update tail in ONE host wait (bann_net.cpp update_branch;
+// net.rs:286-300): bann_hmc_step's trajectory for branch b, then -- stream-ordered, not
+// waited for -- residual_from_target_shift's residual op (residual = target - f_b(final) +
+// add) and the copies of the trajectory status and the final parameters into pinned
+// stages: one stream synchronisation instead of three waits and two synchronous copies
+// (profiles/r06_seq_api.txt).  The same launches in the same order as bann_hmc_step +
+// bann_branch_get_params + residual_from_target_shift, hence the same bits.  stats: sum
+// and sum of squares of the residual before and after the shift.  A recording context and
+// L = 0 take those three calls as they are.
+int hmc_step_tail(bann_ctx* ctx, int32_t b, int32_t L, float max_dh, int32_t step_mode, float factor, const float* eps,
+                  const float* momentum, uint64_t seed, const float* u, float add, int32_t* status_out,
+                  float* params_out, double* stats) {
+  if (!ctx || !ctx->finalized) return fail(ctx, BANN_E_STATE, "not finalized");
+  if (!status_out || !params_out || !stats) return fail(ctx, BANN_E_ARG, "null output");
+  if (L < 1 || ctx->rec_on) {
+    int rc = bann_hmc_step(ctx, &b, 1, L, max_dh, step_mode, factor, eps, momentum, seed, u, status_out, nullptr,
+                           nullptr, nullptr);
+    if (rc) return rc;
+    rc = bann_branch_get_params(ctx, b, params_out);
+    if (rc) return rc;
+    return residual_from_target_shift(ctx, b, add, &stats[0], &stats[1], &stats[2], &stats[3]);
+  }
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  if (ctx->lf_active) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  Plan p;
+  int rc = build_plan(ctx, &b, 1, p, false);
+  if (rc) return rc;
+  rc = traj_prepare(ctx, p, L, max_dh, step_mode, factor, eps, momentum, seed, u);
+  if (rc) return rc;
+  if (ctx->graph_replay) {
+    rc = traj_replay(ctx, p, L);
+  } else {
+    rc = traj_launches(ctx, p, L);
+    mark_predictions(ctx, p, true);
+  }
+  if (rc) return rc;
+  rc = residual_from_target_shift_launch(ctx, b, add);
+  if (rc) return rc;
+  const BranchHost& h = ctx->br[b];
+  CK(hipMemcpyAsync(ctx->h_status + b, ctx->d_status + b, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  CK(hipMemcpyAsync(ctx->h_par_stage, ctx->d_theta + h.dev.p_off, h.P * sizeof(float), hipMemcpyDeviceToHost,
+                    ctx->stream));
+  CK(hipStreamSynchronize(ctx->stream));
+  *status_out = ctx->h_status[b];
+  std::memcpy(params_out, ctx->h_par_stage, h.P * sizeof(float));
+  for (int k = 0; k < 4; ++k) stats[k] = ctx->h_res_stat[k];
+  return BANN_OK;
 }
 
 // hmc_step_joint (branch_sampler.rs:1070-1178): parameters AND precisions

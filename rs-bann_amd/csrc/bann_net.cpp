@@ -27,6 +27,11 @@
 // bann_residual.hip (library-internal): bann_residual_from_target + bann_residual_shift(add) in one launch
 int residual_from_target_shift(bann_ctx* ctx, int32_t b, float add, double* sum, double* sumsq, double* sum_after,
                                double* sumsq_after);
+// bann_api.hip (library-internal): bann_hmc_step + bann_branch_get_params + residual_from_target_shift
+// for one branch with one host wait (stats: sum, sum of squares before / after the shift)
+int hmc_step_tail(bann_ctx* ctx, int32_t b, int32_t L, float max_dh, int32_t step_mode, float factor, const float* eps,
+                  const float* momentum, uint64_t seed, const float* u, float add, int32_t* status_out,
+                  float* params_out, double* stats);
 
 namespace {
 
@@ -879,6 +884,8 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   CKB(bann_branch_set_precisions(t->ctx, b, B.prec.data()));
   CKB(bann_residual_to_target(t->ctx, b));  // net.rs:279-280: fitted to residual + its own prediction
   int32_t status = 0;
+  bool tail = false;  // hmc_step_tail ran: the parameters and the residual statistics are in already
+  double tail_stats[4] = {0.0, 0.0, 0.0, 0.0};
   if (gd) {
     int rc = gradient_descent(t, b, cfg, status);
     if (rc) return rc;
@@ -923,9 +930,16 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
       for (auto& p : dr.mom) p = (float)draw_normal(t);
     }
     dr.u = (float)draw_uniform(t);
-    CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
-                      cfg->hmc_step_size_factor, eps, dev_mom ? nullptr : dr.mom.data(), mseed, &dr.u, &status,
-                      nullptr, nullptr, nullptr));
+    if (!traj) {  // the trajectory, get_params and the residual op below in one host wait
+      CKB(hmc_step_tail(t->ctx, b, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
+                        cfg->hmc_step_size_factor, eps, dev_mom ? nullptr : dr.mom.data(), mseed, &dr.u,
+                        t->ob_bias, &status, B.params.data(), tail_stats));
+      tail = true;
+    } else {
+      CKB(bann_hmc_step(t->ctx, &b, 1, cfg->hmc_integration_length, cfg->hmc_max_hamiltonian_error, mode,
+                        cfg->hmc_step_size_factor, eps, dev_mom ? nullptr : dr.mom.data(), mseed, &dr.u, &status,
+                        nullptr, nullptr, nullptr));
+    }
   }
   if (traj && !gd && !gdj) {  // trajectories file opened in append mode (branch_sampler.rs:1199-1207)
     std::string line;
@@ -936,12 +950,18 @@ int update_branch(bann_net* t, int b, const bann_mcmc_cfg* cfg, bool traj, const
   ++t->ns;  // TrainingStats::add_hmc_step_result (train_stats.rs:46-53)
   if (status == BANN_ACCEPTED) ++t->nacc;
   if (status == BANN_REJECTED_EARLY) ++t->nearly;
-  CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
   // net.rs:292-300: residual = target - f_b(final) (accepted: y_pred; rejected: prev_pred),
   // and the output-bias shift of net.rs:321 (residual += bias) in the same launch: nothing
   // between the two touches the residual (sr_bias: its sum after the shift)
   double sr = 0.0, sr_bias = 0.0;
-  CKB(residual_from_target_shift(t->ctx, b, t->ob_bias, &sr, &t->rss_cur, &sr_bias, nullptr));
+  if (tail) {
+    sr = tail_stats[0];
+    t->rss_cur = tail_stats[1];
+    sr_bias = tail_stats[2];
+  } else {
+    CKB(bann_branch_get_params(t->ctx, b, B.params.data()));
+    CKB(residual_from_target_shift(t->ctx, b, t->ob_bias, &sr, &t->rss_cur, &sr_bias, nullptr));
+  }
   if (status == BANN_ACCEPTED) update_lpd(t, b, others);
   // to_cfg + GlobalParams::update_from_branch_cfg (net.rs:303-305, params.rs:41-56)
   B.ows_reg_sum = (float)(others + B.out_stat());

@@ -189,16 +189,18 @@ int ensure_predictions(bann_ctx* ctx, const int32_t* branches, int32_t nb) {
   return run_forward(ctx, p);
 }
 
+// defer: the statistics are written to the pinned h_res_stat but not waited for (the
+// caller synchronises the stream later: hmc_step_tail)
 static int residual_op(bann_ctx* ctx, int op, int b, const float* d_y, float add, const int32_t* d_list, int nb,
-                       double* sum, double* sumsq, double* after = nullptr) {
+                       double* sum, double* sumsq, double* after = nullptr, bool defer = false) {
   const int64_t nblk = res_blocks(ctx->n);
-  const bool want = sum || sumsq || after;
+  const bool want = sum || sumsq || after || defer;
   hipLaunchKernelGGL(k_residual_op, dim3((unsigned)nblk), dim3(RES_BLK), 0, ctx->stream, ctx->st, ctx->d_res, op, b,
                      d_y, add, d_list, nb, ctx->d_res_part,
                      reinterpret_cast<unsigned*>(ctx->d_res_part + 4 * nblk + 4), ctx->d_res_part + 4 * nblk,
                      want ? ctx->d_res_stat_host : nullptr);
   CK(hipGetLastError());
-  if (want) {
+  if (want && !defer) {
     CK(hipStreamSynchronize(ctx->stream));
     if (sum) *sum = ctx->h_res_stat[0];
     if (sumsq) *sumsq = ctx->h_res_stat[1];
@@ -320,6 +322,18 @@ extern "C" int bann_residual_from_target(bann_ctx* ctx, int32_t b, double* sum, 
 // follows it (net.rs:319-321) in one launch: residual = (y_b - f_b) + add; stats of the
 // residual before (sum, sum of squares) and after the shift -- the bits of
 // bann_residual_from_target followed by bann_residual_shift(add)
+// the same residual op launched without a wait: its statistics (sum, sum of squares
+// before and after the shift) are in ctx->h_res_stat once the stream has drained
+int residual_from_target_shift_launch(bann_ctx* ctx, int32_t b, float add) {
+  int rc = ensure_residual(ctx);
+  if (rc) return rc;
+  if (!check_branch(ctx, b)) return fail(ctx, BANN_E_ARG, "bad branch");
+  if (!session_free(ctx)) return fail(ctx, BANN_E_STATE, "a leapfrog session is active");
+  rc = ensure_predictions(ctx, &b, 1);
+  if (rc) return rc;
+  return residual_op(ctx, 4, b, nullptr, add, nullptr, 0, nullptr, nullptr, nullptr, true);
+}
+
 int residual_from_target_shift(bann_ctx* ctx, int32_t b, float add, double* sum, double* sumsq, double* sum_after,
                                double* sumsq_after) {
   int rc = ensure_residual(ctx);

@@ -120,6 +120,7 @@ struct bann_ctx {
   float* d_delta = nullptr;       // n floats: residual change of the last trajectory (host-copy variant)
   float* d_delta_part = nullptr;  // per-branch-slice partial rows of the residual change
   int32_t* h_status = nullptr;    // pinned host mirrors (trajectory status, residual change)
+  float* h_par_stage = nullptr;   // pinned: one branch's parameters (hmc_step_tail), max P floats
   float* h_delta = nullptr;
   float *d_y = nullptr, *d_pred = nullptr, *d_scr = nullptr, *d_eprec = nullptr, *d_u = nullptr;
   double *d_h0 = nullptr, *d_htrace = nullptr, *d_ld = nullptr, *d_rss = nullptr;
@@ -262,6 +263,13 @@ void tm_mark_follow(bann_ctx* ctx, int32_t kind);
 int tm_resolve(bann_ctx* ctx);  // after the stream has drained
 // bann_dist.hip: the network sampler's device buffers, allocated once at bann_finalize
 // (no allocation or synchronous upload inside a collective trajectory)
+// the sequential driver's branch-update tail (bann_api.hip / bann_residual.hip)
+int residual_from_target_shift(bann_ctx* ctx, int32_t b, float add, double* sum, double* sumsq, double* sum_after,
+                               double* sumsq_after);
+int residual_from_target_shift_launch(bann_ctx* ctx, int32_t b, float add);
+int hmc_step_tail(bann_ctx* ctx, int32_t b, int32_t L, float max_dh, int32_t step_mode, float factor, const float* eps,
+                  const float* momentum, uint64_t seed, const float* u, float add, int32_t* status_out,
+                  float* params_out, double* stats);
 int net_buffers_init(bann_ctx* ctx);
 // network mode: k_forward_gsum's items for a persistent fx-only plan of 8-chunk branches
 int build_net_groups(bann_ctx* ctx, Plan& p);
