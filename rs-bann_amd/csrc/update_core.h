@@ -405,6 +405,7 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
     const int nk = w0 - k0 < 4 ? w0 - k0 : 4;
     float mx[R][4];
     double cs[R][4];
+    float wps[R][MPT][4];  // W0 / sigma, kept for the digit pass (one division per value)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
 #pragma unroll
@@ -415,11 +416,14 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
 #pragma unroll
       for (int c = 0; c < MPT; ++c) {
         const int j = t + r * NT + c * NV_T;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wps[r][c][q] = 0.f;
         if (j >= m) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
           if (q < nk) {
             const float wp = sgs[r][c] > 0.f ? W0[(k0 + q) * m + j] / sgs[r][c] : 0.f;
+            wps[r][c][q] = wp;
             mx[r][q] = fmaxf(mx[r][q], fabsf(wp));
             cs[r][q] += (double)mus[r][c] * (double)wp;
           }
@@ -441,9 +445,11 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
           s_cs[q][wv + r * (NT / 64)] = cs[r][q];
         }
     __syncthreads();
-    double inv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    // thread q combines column q's per-wave max and sum (wave order) and publishes the
+    // scale: four threads read the NV_T / 64 partials instead of every thread
+    __shared__ float s_inv[4];
+    if (t < 4) {
+      const int q = t;
       float M = s_mx[q][0];
       double C = s_cs[q][0];
       for (int w = 1; w < NV_T / 64; ++w) {
@@ -456,12 +462,16 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
         frexpf(M / 127.f, &e);
         sc = ldexpf(1.f, e);
       }
-      inv[q] = 1.0 / (double)sc;
-      if (t == 0 && q < nk) {
+      s_inv[q] = 1.f / sc;  // a power of two: exact
+      if (q < nk) {
         st.fc[b].scale[k0 + q] = sc;
         st.fc[b].c0[k0 + q] = (float)((double)b0[k0 + q] - C);
       }
     }
+    __syncthreads();
+    float inv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) inv[q] = s_inv[q];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -473,14 +483,15 @@ __device__ void update_small(const DevState& st, int b, const BranchDev& bd, int
         for (int q = 0; q < 4; ++q) {
           if (q >= nk) continue;
           const int k = k0 + q;
-          const float wp = sgs[r][c] > 0.f ? W0[k * m + j] / sgs[r][c] : 0.f;
-          double v = (double)wp * inv[q];  // |v| <= 127, exact (power-of-two scale)
+          // |v| <= 127 and every step below is exact in f32 (a power-of-two scale, the
+          // nearest integer's remainder, times 128): the digits of refresh_fused_const's f64 chain
+          float v = wps[r][c][q] * inv[q];
           int8_t dq[4];
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
-            const double rr = rint(v);
+            const float rr = rintf(v);
             dq[d] = (int8_t)rr;
-            v = (v - rr) * 128.0;
+            v = (v - rr) * 128.f;
           }
 #pragma unroll
           for (int d = 0; d < 4; ++d)
